@@ -1,0 +1,250 @@
+"""Parity of the gfx950 path (through the C-ABI) with the reference.
+
+Expected values come from the golden vectors the REAL reference produced
+(tests/golden/*.json); per-frame status bits, which the reference does not
+compute, come from the oracle (oracle/xyws_oracle.c) run on the same input.
+Bar: bit-exact bytes, frames and carries.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+import streams
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+MODES = {"fused": False, "serial": True}
+
+
+@pytest.fixture(scope="module")
+def ws():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from xynet_amd import websocket
+    return websocket
+
+
+def dev_bytes(src: bytes, offset=0, pad=32):
+    """src placed at byte `offset` of a guarded device buffer; returns (view, whole)."""
+    whole = torch.full((offset + len(src) + pad,), 0xA5, dtype=torch.uint8, device="cuda")
+    if src:
+        whole[offset:offset + len(src)] = torch.frombuffer(bytearray(src), dtype=torch.uint8).cuda()
+    return whole[offset:offset + len(src)], whole
+
+
+def host(t):
+    return t.cpu().numpy().tobytes()
+
+
+def frames_list(fr, with_status=False):
+    out = []
+    for f in fr:
+        x = [f.frame_off, f.payload_off, f.payload_len, bytes(f.key).hex(), f.flags, f.hdr_len,
+             f.status if with_status else f.status & 1]
+        out.append(x)
+    return out
+
+
+def carry_list(c):
+    return [c.payload_remaining, c.phase, c.frames_total, bytes(c.key).hex(), c.hdr_len,
+            bytes(c.hdr[:c.hdr_len]).hex()]
+
+
+# --------------------------------------------------------------------------- unmask
+def test_unmask_golden_vectors(ws, oracle):
+    for v in load_golden("unmask.json")["vectors"]:
+        rng = streams.SplitMix(v["seed"])
+        key = rng.next() & 0xFFFFFFFF
+        src = rng.bytes(v["n"])
+        for off in (0, 1, 3, 7, 13):
+            view, whole = dev_bytes(src, off)
+            ret = ws.websocket_mask(view, key, v["phase"])
+            assert ret == v["ret"]
+            out = host(whole)
+            assert out[:off] == b"\xa5" * off and out[off + v["n"]:] == b"\xa5" * 32
+            got = out[off:off + v["n"]]
+            if "out" in v:
+                assert got.hex() == v["out"], (v["n"], v["phase"], off)
+            else:
+                assert oracle.digest(np.frombuffer(got, np.uint8)) == v["out_digest"]
+
+
+def test_unmask_is_involution_large(ws):
+    n = (64 << 20) + 5
+    t = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    ref = t.clone()
+    assert ws.websocket_mask(t, 0xDEADBEEF, 3) == n + 3
+    assert not torch.equal(t, ref)
+    ws.websocket_mask(t, 0xDEADBEEF, 3)
+    assert torch.equal(t, ref)
+
+
+# --------------------------------------------------------------------------- stream
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("name", streams.EDGE_CASES)
+def test_stream_edge_cases(ws, oracle, name, mode):
+    g = load_golden("streams.json")["cases"][name]
+    src = streams.case_bytes(name)
+    for off in (0, 5):
+        view, whole = dev_bytes(src, off)
+        dec = ws.frame_decoder(serial=MODES[mode])
+        cap = g["nframes"] + 4
+        r = dec.decode(view, cap=cap)
+        assert r.nframes == g["nframes"]
+        out = host(whole)
+        assert out[:off] == b"\xa5" * off and out[off + len(src):] == b"\xa5" * 32
+        got = np.frombuffer(out[off:off + len(src)], np.uint8)
+        assert oracle.digest(got) == g["out_digest"], (name, mode, off)
+        if "out" in g:
+            assert got.tobytes().hex() == g["out"]
+        fr = r.frames()
+        assert frames_list(fr) == g["frames"]
+        assert carry_list(dec.carry()) == g["carry"]
+        # informational status bits: same as the oracle on the same input
+        ob = np.frombuffer(src, np.uint8).copy() if src else np.zeros(0, np.uint8)
+        ofr, _, _ = oracle.decode_stream(ob)
+        assert frames_list(fr, True) == frames_list(ofr, True)
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("name", ["lengths", "tiny_frames", "random_frames_200", "fragments",
+                                  "trunc_hdr_9", "len_msb", "random_bytes_3000"])
+def test_stream_split_with_carry(ws, name, mode):
+    g = load_golden("streams.json")["cases"][name]
+    src = streams.case_bytes(name)
+    for s in g["splits"]:
+        k = s["k"]
+        a, wa = dev_bytes(src[:k])
+        b, wb = dev_bytes(src[k:])
+        dec = ws.frame_decoder(serial=MODES[mode])
+        ra = dec.decode(a, cap=g["nframes"] + 2)
+        assert ra.nframes == s["n1"]
+        assert carry_list(dec.carry()) == s["carry_mid"], (name, k)
+        rb = dec.decode(b, cap=g["nframes"] + 2)
+        assert ra.nframes + rb.nframes == g["nframes"]
+        assert carry_list(dec.carry()) == g["carry"]
+        joined = host(a) + host(b)
+        if "out" in g:
+            assert joined.hex() == g["out"], (name, k)
+        fb = frames_list(rb.frames())
+        assert [[x[0] + k, x[1] + k] + x[2:] for x in fb] == g["frames"][s["n1"]:]
+
+
+def test_fuzz_random_streams_vs_oracle(ws, oracle):
+    """Random frame soups + random cut points, GPU (fused) vs oracle."""
+    rng = streams.SplitMix(0xF022)
+    for it in range(40):
+        n = 1 + rng.below(300)
+        src = streams.case_bytes(f"random_frames_{n}") if it % 2 else streams.SplitMix(it).bytes(
+            rng.below(200000))
+        cuts = sorted(set([0, len(src)] + [rng.below(len(src) + 1) for _ in range(rng.below(4))]))
+        dec = ws.frame_decoder()
+        carry = None
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            piece = src[a:b]
+            view, _ = dev_bytes(piece)
+            r = dec.decode(view, cap=len(piece) + 2)
+            ob = np.frombuffer(piece, np.uint8).copy() if piece else np.zeros(0, np.uint8)
+            ofr, carry, on = oracle.decode_stream(ob, carry_in=carry)
+            assert r.nframes == on, (it, a, b)
+            assert host(view) == ob.tobytes(), (it, a, b)
+            assert frames_list(r.frames(), True) == frames_list(ofr, True)
+            assert carry_list(dec.carry()) == carry_list(carry)
+
+
+# --------------------------------------------------------------------------- indexed
+def test_indexed_matches_golden(ws):
+    g = load_golden("streams.json")["cases"]["lengths"]
+    src = streams.case_bytes("lengths")
+    view, _ = dev_bytes(src, 3)
+    r = ws.decode_indexed(view, [f[0] for f in g["frames"]])
+    assert host(view).hex() == g.get("out", host(view).hex())
+    from conftest import GOLDEN  # noqa: F401
+    assert frames_list(r.frames()) == g["frames"]
+
+
+def test_indexed_overlap_and_tail(ws, oracle):
+    src = streams.case_bytes("random_frames_40")
+    starts = [0, 5, 5, 100, 2000, len(src) - 3, len(src) + 10]
+    view, _ = dev_bytes(src)
+    r = ws.decode_indexed(view, starts)
+    ob = np.frombuffer(src, np.uint8).copy()
+    ofr = oracle.decode_indexed(ob, starts)
+    assert host(view) == ob.tobytes()
+    assert frames_list(r.frames(), True) == frames_list(ofr, True)
+
+
+# --------------------------------------------------------------------------- parser mirror
+def test_parser_mirror_reference_cases(ws):
+    """test/websocket_frame_test.cpp through the device-backed parser."""
+    g = load_golden("frame_header.json")
+    for c in g["cases"]:
+        hb = bytes.fromhex(c["header"])
+        p = ws.websocket_frame_header_parser()
+        view, _ = dev_bytes(hb)
+        assert p.parse(view) == c["ret"]
+        f, m, l = p.result()
+        assert (int(f), l) == (c["r_flags"], c["r_length"])
+        assert ws.websocket_frame_header(c["flags"], c["length"]).span().hex() == c["header"]
+    hb = bytes.fromhex(g["cases"][-2]["header"])  # FIN|MASK|PING, 120
+    for s in g["splits"]:
+        k = s["split"]
+        p = ws.websocket_frame_header_parser()
+        a, _ = dev_bytes(hb[:k])
+        b, _ = dev_bytes(hb[k:])
+        assert p.parse(a) == ws.npos
+        assert p.parse(b) == s["ret2"]
+        assert (int(p.flags()), p.length()) == (s["r_flags"], s["r_length"])
+
+
+# --------------------------------------------------------------------------- full configs
+def tools_batch(name):
+    from xynet_amd import _lib
+    T = _lib.load_tools()
+    c = load_golden("configs.json")["configs"][name]
+    buf = torch.empty(c["size"], dtype=torch.uint8, device="cuda")
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if c["kind"] == "uniform":
+        assert T.xyws_tools_fill_uniform(C.c_void_p(buf.data_ptr()), c["nframes"], c["payload"],
+                                         c["b0"], c["seed"], s) == 0
+    else:
+        from xynet_amd._lib import C as _C  # noqa: F401
+        tot = C.c_uint64()
+        n = T.xyws_tools_mixed_table(c["seed"], c["target"], None, 0, C.byref(tot))
+        tab = torch.empty(n * 32, dtype=torch.uint8)
+        T.xyws_tools_mixed_table(c["seed"], c["target"], C.c_void_p(tab.data_ptr()), n, C.byref(tot))
+        assert tot.value == c["size"]
+        dtab = tab.cuda()
+        assert T.xyws_tools_fill_mixed(C.c_void_p(buf.data_ptr()), c["size"],
+                                       C.c_void_p(dtab.data_ptr()), n, c["seed"], s) == 0
+    return buf, c
+
+
+def dev_digest(buf):
+    from xynet_amd import _lib
+    T = _lib.load_tools()
+    out = torch.zeros(2, dtype=torch.int64, device="cuda")
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert T.xyws_tools_digest(C.c_void_p(buf.data_ptr()), buf.numel(),
+                               C.c_void_p(out.data_ptr()), C.c_void_p(out.data_ptr() + 8), s) == 0
+    return int(out[0].item()) & ((1 << 64) - 1)
+
+
+@pytest.mark.parametrize("name", ["t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m", "c1_text_4k",
+                                  "c2_bin_256", "c3_bin_64k", "c4_mixed", "c5_shard0", "c5_shard7"])
+def test_config_batches(ws, name):
+    buf, c = tools_batch(name)
+    assert dev_digest(buf) == c["in_digest"], "device generator disagrees with the host spec"
+    dec = ws.frame_decoder()
+    r = dec.decode(buf, cap=16)
+    assert r.nframes == c["decoded_frames"]
+    assert dev_digest(buf) == c["out_digest"]
+    assert carry_list(dec.carry()) == c["carry"]
+    assert frames_list(r.frames()[:4]) == c["first_frames"]
+    assert dec.ctx.last_device_error() == 0
+    del buf
+    torch.cuda.empty_cache()

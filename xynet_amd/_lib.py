@@ -1,0 +1,114 @@
+"""ctypes binding of libxyws.so (include/xyws.h) and libxyws_tools.so.
+
+The decode path has no CPU fallback: if the in-tree HIP library is missing or a
+device is absent, calls raise XywsError instead of computing anything on the
+host.
+"""
+import ctypes as C
+import os
+import re
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+HEADER = os.path.join(ROOT, "include", "xyws.h")
+
+XYWS_OK = 0
+ERRORS = {-1: "invalid argument", -2: "HIP runtime error", -3: "device allocation failed",
+          -4: "scratch capacity exceeded", -5: "device-side error"}
+
+
+class XywsError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        super().__init__(f"xyws error {code} ({ERRORS.get(code, '?')}){': ' + what if what else ''}")
+
+
+class Frame(C.Structure):
+    """xyws_frame (include/xyws.h), 32 bytes."""
+    _fields_ = [("frame_off", C.c_int64), ("payload_off", C.c_int64),
+                ("payload_len", C.c_uint64), ("key", C.c_uint8 * 4),
+                ("flags", C.c_uint8), ("hdr_len", C.c_uint8),
+                ("status", C.c_uint8), ("reserved", C.c_uint8)]
+
+
+class Carry(C.Structure):
+    """xyws_carry (include/xyws.h), 64 bytes."""
+    _fields_ = [("payload_remaining", C.c_uint64), ("phase", C.c_uint64),
+                ("frames_total", C.c_uint64), ("key", C.c_uint8 * 4),
+                ("hdr_len", C.c_uint8), ("hdr", C.c_uint8 * 14),
+                ("reserved", C.c_uint8 * 21)]
+
+
+assert C.sizeof(Frame) == 32 and C.sizeof(Carry) == 64
+
+_lib = None
+_tools = None
+
+
+def declared_symbols(header=HEADER):
+    """Function names declared in include/xyws.h."""
+    src = open(header).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*|uint64_t|void)\s+(xyws_\w+)\s*\(",
+                                 src, re.M)))
+
+
+def lib_path(name="libxyws.so"):
+    return os.path.join(PKG, name)
+
+
+def load():
+    """Load libxyws.so (raises if it was not built: no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not os.path.exists(path):
+        raise XywsError(-2, f"{path} missing: build it with `python -m xynet_amd.build`")
+    L = C.CDLL(path)
+    u64, u32, u8, vp, i32 = C.c_uint64, C.c_uint32, C.c_uint8, C.c_void_p, C.c_int
+    L.xyws_abi_version.restype = i32
+    L.xyws_strerror.restype = C.c_char_p
+    L.xyws_strerror.argtypes = [i32]
+    L.xyws_ctx_create.restype = i32
+    L.xyws_ctx_create.argtypes = [i32, C.POINTER(vp)]
+    L.xyws_ctx_destroy.restype = i32
+    L.xyws_ctx_destroy.argtypes = [vp]
+    L.xyws_ctx_reserve.restype = i32
+    L.xyws_ctx_reserve.argtypes = [vp, u64, u64]
+    L.xyws_ctx_last_device_error.restype = i32
+    L.xyws_ctx_last_device_error.argtypes = [vp, C.POINTER(u32)]
+    L.xyws_unmask.restype = i32
+    L.xyws_unmask.argtypes = [vp, vp, u64, vp, u64, C.POINTER(u64), vp]
+    L.xyws_decode_indexed.restype = i32
+    L.xyws_decode_indexed.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp]
+    L.xyws_decode_stream.restype = i32
+    L.xyws_decode_stream.argtypes = [vp, vp, u64, vp, vp, vp, u64, vp, u32, vp]
+    _lib = L
+    return L
+
+
+def load_tools():
+    global _tools
+    if _tools is not None:
+        return _tools
+    path = lib_path("libxyws_tools.so")
+    if not os.path.exists(path):
+        raise XywsError(-2, f"{path} missing: build it with `python -m xynet_amd.build`")
+    T = C.CDLL(path)
+    u64, u8, vp, i32 = C.c_uint64, C.c_uint8, C.c_void_p, C.c_int
+    T.xyws_tools_fill_uniform.restype = i32
+    T.xyws_tools_fill_uniform.argtypes = [vp, u64, u64, u8, u64, vp]
+    T.xyws_tools_mixed_table.restype = u64
+    T.xyws_tools_mixed_table.argtypes = [u64, u64, vp, u64, C.POINTER(u64)]
+    T.xyws_tools_fill_mixed.restype = i32
+    T.xyws_tools_fill_mixed.argtypes = [vp, u64, vp, u64, u64, vp]
+    T.xyws_tools_digest.restype = i32
+    T.xyws_tools_digest.argtypes = [vp, u64, vp, vp, vp]
+    _tools = T
+    return T
+
+
+def check(rc, what=""):
+    if rc != XYWS_OK:
+        raise XywsError(rc, what)
+    return rc

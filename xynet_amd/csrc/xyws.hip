@@ -1,0 +1,499 @@
+// xyws.hip — gfx950 WebSocket frame decode: kernels + the C-ABI of include/xyws.h.
+//
+// Hot path of xuanyi-fu/xynet re-designed for MI355X (paths relative to the
+// reference tree):
+//   websocket_mask            include/xynet/http/websocket_frame_mask.h:6-25
+//   header parse              include/xynet/http/websocket_frame_header.h:305-385
+//   per-frame driver          example/include/common/websocket.h:110-134
+//
+// Kernels in this file
+//   k_unmask_range   xyws_unmask: in-place XOR of one contiguous range, 16 B/lane.
+//   k_parse_indexed  xyws_decode_indexed, step 1: one lane per caller-given start.
+//   k_stream_serial  xyws_decode_stream with XYWS_OPT_SERIAL_SCAN: one-lane
+//                    boundary chase (exact, latency bound; debug/reference shape).
+//   k_unmask_tiles   step 2 of both: byte tiles of 16 KiB per workgroup, each
+//                    lane XORs 4 x 16 B with the covering frames' rotated keys.
+//   k_stream_fused   (xyws_stream.hip) the default stream decoder: one pass,
+//                    boundary discovery by tile + decoupled look-back.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdlib.h>
+#include <mutex>
+
+#include "xyws.h"
+#include "xyws_device.h"
+#include "xyws_stream.h"
+
+#ifndef XYWS_HAVE_FUSED
+#define XYWS_HAVE_FUSED 0
+#endif
+
+// ---------------------------------------------------------------------------
+// Frame table (device scratch, SoA) consumed by k_unmask_tiles. Entries are
+// sorted by position and non-overlapping; [ps, pe) is the payload range to
+// unmask (already clipped), kw the key word for 4-byte-aligned positions.
+struct frame_table {
+  uint64_t* start;
+  uint64_t* ps;
+  uint64_t* pe;
+  uint32_t* kw;
+  uint64_t* count;  // number of valid entries (device)
+};
+
+#define UNMASK_TILE 16384u
+#define UNMASK_THREADS 256u
+#define UNMASK_LDS_FRAMES 512u
+
+// ---------------------------------------------------------------------------
+// k_unmask_range: dev[j] ^= K[(ph + j) % 4] over positions [lo, hi).
+// kw = aligned_key(K, lo, ph). Interior 16-byte chunks: one dwordx4 load, 4
+// XORs, one dwordx4 store per lane; the two edge chunks store only their
+// in-range bytes.
+__global__ void __launch_bounds__(256) k_unmask_range(uint8_t* __restrict__ base, uint64_t lo,
+                                                      uint64_t hi, uint32_t kw) {
+  const uint64_t c0 = lo >> 4, c1 = (hi + 15) >> 4;  // chunk range
+  const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+  u32x4* __restrict__ p = reinterpret_cast<u32x4*>(base);
+  for (uint64_t c = c0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < c1; c += nthreads) {
+    const uint64_t a = c << 4;
+    if (a >= lo && a + 16 <= hi) {
+      u32x4 v = __builtin_nontemporal_load(p + c);
+      v.x ^= kw; v.y ^= kw; v.z ^= kw; v.w ^= kw;
+      __builtin_nontemporal_store(v, p + c);
+    } else {
+      for (uint32_t t = 0; t < 16; t++) {
+        uint64_t q = a + t;
+        if (q >= lo && q < hi) base[q] ^= (uint8_t)(kw >> (8u * (t & 3u)));
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_parse_indexed: one lane per frame start (ascending, caller supplied).
+__global__ void __launch_bounds__(256) k_parse_indexed(const uint8_t* __restrict__ base, uint64_t lo,
+                                                       uint64_t hi, const uint64_t* __restrict__ starts,
+                                                       uint64_t n, frame_table tab,
+                                                       xyws_frame* __restrict__ frames) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t len = hi - lo;
+  const uint64_t s_rel = starts[i];
+  const uint64_t s = lo + (s_rel < len ? s_rel : len);
+  uint8_t hb[XYWS_MAX_FRAME_HEADER_SIZE];
+  uint32_t avail = 0;
+  for (; avail < XYWS_MAX_FRAME_HEADER_SIZE && s + avail < hi; avail++) hb[avail] = base[s + avail];
+  hdr_info h = parse_header_bytes(hb, avail);
+  xyws_frame f;
+  f.frame_off = (int64_t)s_rel;
+  f.payload_off = (int64_t)s_rel;
+  f.payload_len = 0;
+  f.flags = 0; f.hdr_len = 0; f.status = 0; f.reserved = 0;
+  f.key[0] = f.key[1] = f.key[2] = f.key[3] = 0;
+  uint64_t ps = s, pe = s;
+  if (h.hlen && s_rel < len) {
+    ps = s + h.hlen;
+    uint64_t end = sat_add(ps, h.plen);
+    pe = end < hi ? end : hi;
+    uint8_t st = h.status;
+    if (end > hi) st |= XYWS_ST_PAYLOAD_INCOMPLETE;
+    if (i + 1 < n) {
+      uint64_t nx_rel = starts[i + 1];
+      uint64_t nx = lo + (nx_rel < len ? nx_rel : len);
+      if (end > nx) st |= XYWS_ST_OVERLAP;
+      if (pe > nx) pe = nx;
+    }
+    if (pe < ps) pe = ps;
+    f.payload_off = (int64_t)(s_rel + h.hlen);
+    f.payload_len = h.plen;
+    f.key[0] = (uint8_t)h.key; f.key[1] = (uint8_t)(h.key >> 8);
+    f.key[2] = (uint8_t)(h.key >> 16); f.key[3] = (uint8_t)(h.key >> 24);
+    f.flags = h.flags;
+    f.hdr_len = (uint8_t)h.hlen;
+    f.status = st;
+  }
+  tab.start[i] = s;
+  tab.ps[i] = ps;
+  tab.pe[i] = pe;
+  tab.kw[i] = aligned_key(h.key, ps, 0);
+  if (i == 0) *tab.count = n;
+  if (frames) frames[i] = f;
+}
+
+// ---------------------------------------------------------------------------
+// k_stream_serial: exact one-lane chase (XYWS_OPT_SERIAL_SCAN). Writes the
+// frame table, descriptors, count and carry. Latency bound by design: it is
+// the simplest statement of the stream semantics on the device.
+__global__ void k_stream_serial(const uint8_t* __restrict__ base, uint64_t lo, uint64_t hi,
+                                const xyws_carry* __restrict__ cin, xyws_carry* __restrict__ cout,
+                                frame_table tab, uint64_t tab_cap, xyws_frame* __restrict__ frames,
+                                uint64_t cap, uint64_t* __restrict__ nframes,
+                                uint32_t* __restrict__ err) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  xyws_carry c;
+  if (cin) c = *cin; else memset(&c, 0, sizeof c);
+  uint64_t pos = lo, nt = 0, nf = 0;
+  if (c.payload_remaining) {
+    uint64_t take = c.payload_remaining < hi - lo ? c.payload_remaining : hi - lo;
+    uint32_t k = (uint32_t)c.key[0] | ((uint32_t)c.key[1] << 8) | ((uint32_t)c.key[2] << 16) |
+                 ((uint32_t)c.key[3] << 24);
+    tab.start[nt] = lo; tab.ps[nt] = lo; tab.pe[nt] = lo + take;
+    tab.kw[nt] = aligned_key(k, lo, c.phase);
+    nt++;
+    c.phase += take;
+    c.payload_remaining -= take;
+    pos = lo + take;
+    if (!c.payload_remaining) { c.phase = 0; c.key[0] = c.key[1] = c.key[2] = c.key[3] = 0; }
+  }
+  while (pos < hi) {
+    uint8_t hb[XYWS_MAX_FRAME_HEADER_SIZE];
+    uint32_t h0 = c.hdr_len, avail = h0;
+    for (uint32_t i = 0; i < h0; i++) hb[i] = c.hdr[i];
+    for (; avail < XYWS_MAX_FRAME_HEADER_SIZE && pos + (avail - h0) < hi; avail++)
+      hb[avail] = base[pos + (avail - h0)];
+    hdr_info h = parse_header_bytes(hb, avail);
+    if (!h.hlen) {  // incomplete header: carry its bytes
+      for (uint32_t i = h0; i < avail; i++) c.hdr[i] = hb[i];
+      c.hdr_len = (uint8_t)avail;
+      pos = hi;
+      break;
+    }
+    const uint64_t ps = pos + (h.hlen - h0);
+    const uint64_t end = sat_add(ps, h.plen);
+    uint8_t st = h.status;
+    uint64_t pe = end;
+    if (end > hi) {
+      pe = hi;
+      st |= XYWS_ST_PAYLOAD_INCOMPLETE;
+      c.payload_remaining = h.plen - (hi - ps);
+      c.phase = hi - ps;
+      c.key[0] = (uint8_t)h.key; c.key[1] = (uint8_t)(h.key >> 8);
+      c.key[2] = (uint8_t)(h.key >> 16); c.key[3] = (uint8_t)(h.key >> 24);
+    }
+    if (nt >= tab_cap) { atomicOr(err, 1u); break; }
+    tab.start[nt] = pos; tab.ps[nt] = ps; tab.pe[nt] = pe; tab.kw[nt] = aligned_key(h.key, ps, 0);
+    nt++;
+    if (frames && nf < cap) {
+      xyws_frame f;
+      f.frame_off = (int64_t)(pos - lo) - (int64_t)h0;
+      f.payload_off = (int64_t)(ps - lo);
+      f.payload_len = h.plen;
+      f.key[0] = (uint8_t)h.key; f.key[1] = (uint8_t)(h.key >> 8);
+      f.key[2] = (uint8_t)(h.key >> 16); f.key[3] = (uint8_t)(h.key >> 24);
+      f.flags = h.flags; f.hdr_len = (uint8_t)h.hlen; f.status = st; f.reserved = 0;
+      frames[nf] = f;
+    }
+    nf++;
+    c.hdr_len = 0;
+    for (int i = 0; i < 14; i++) c.hdr[i] = 0;
+    pos = pe;
+  }
+  c.frames_total += nf;
+  *tab.count = nt;
+  if (nframes) *nframes = nf;
+  if (cout) *cout = c;
+}
+
+// ---------------------------------------------------------------------------
+// k_unmask_tiles: 16 KiB byte tiles over [lo, hi). Each workgroup stages the
+// frame-table slice that touches its tile in LDS; each lane handles four
+// 16-byte chunks (coalesced: chunk = tile*1024 + k*256 + lane).
+__global__ void __launch_bounds__(UNMASK_THREADS) k_unmask_tiles(uint8_t* __restrict__ base, uint64_t lo,
+                                                                 uint64_t hi, frame_table tab) {
+  __shared__ uint64_t s_ps[UNMASK_LDS_FRAMES], s_pe[UNMASK_LDS_FRAMES];
+  __shared__ uint32_t s_kw[UNMASK_LDS_FRAMES];
+  __shared__ uint64_t s_f0, s_f1;
+  const uint64_t n = *tab.count;
+  const uint64_t t0 = lo & ~(uint64_t)(UNMASK_TILE - 1);
+  const uint64_t ntiles = (hi - t0 + UNMASK_TILE - 1) / UNMASK_TILE;
+  u32x4* __restrict__ p = reinterpret_cast<u32x4*>(base);
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t ts = t0 + tile * UNMASK_TILE, te = ts + UNMASK_TILE;
+    if (threadIdx.x == 0) {
+      // f0: first frame with pe > ts; f1: first frame with ps >= te (pe, ps non-decreasing)
+      uint64_t a = 0, b = n;
+      while (a < b) { uint64_t m = (a + b) >> 1; if (tab.pe[m] > ts) b = m; else a = m + 1; }
+      s_f0 = a;
+      b = n;
+      while (a < b) { uint64_t m = (a + b) >> 1; if (tab.ps[m] >= te) b = m; else a = m + 1; }
+      s_f1 = a;
+    }
+    __syncthreads();
+    const uint64_t f0 = s_f0, f1 = s_f1, nf = f1 - f0;
+    const bool in_lds = nf <= UNMASK_LDS_FRAMES;
+    if (in_lds) {
+      for (uint64_t i = threadIdx.x; i < nf; i += blockDim.x) {
+        s_ps[i] = tab.ps[f0 + i]; s_pe[i] = tab.pe[f0 + i]; s_kw[i] = tab.kw[f0 + i];
+      }
+    }
+    __syncthreads();
+    if (nf) {
+#pragma unroll
+      for (uint32_t k = 0; k < UNMASK_TILE / (16u * UNMASK_THREADS); k++) {
+        const uint64_t a = ts + ((uint64_t)k * UNMASK_THREADS + threadIdx.x) * 16u;
+        if (a + 16 <= lo || a >= hi) continue;
+        // first frame with pe > a
+        uint64_t g;
+        {
+          uint64_t x = 0, y = nf;
+          while (x < y) {
+            uint64_t m = (x + y) >> 1;
+            uint64_t pem = in_lds ? s_pe[m] : tab.pe[f0 + m];
+            if (pem > a) y = m; else x = m + 1;
+          }
+          g = x;
+        }
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (; g < nf; g++) {
+          const uint64_t ps = in_lds ? s_ps[g] : tab.ps[f0 + g];
+          if (ps >= a + 16) break;
+          const uint64_t pe = in_lds ? s_pe[g] : tab.pe[f0 + g];
+          const uint32_t kw = in_lds ? s_kw[g] : tab.kw[f0 + g];
+#pragma unroll
+          for (uint32_t d = 0; d < 4; d++) w[d] |= kw & range_mask(a + 4 * d, ps, pe);
+        }
+        if ((w[0] | w[1] | w[2] | w[3]) == 0u) continue;
+        if (a >= lo && a + 16 <= hi) {
+          u32x4 v = p[a >> 4];
+          v.x ^= w[0]; v.y ^= w[1]; v.z ^= w[2]; v.w ^= w[3];
+          p[a >> 4] = v;
+        } else {
+          for (uint32_t t = 0; t < 16; t++) {
+            uint64_t q = a + t;
+            uint8_t x = (uint8_t)(w[t >> 2] >> (8u * (t & 3u)));
+            if (q >= lo && q < hi && x) base[q] ^= x;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+struct xyws_ctx {
+  int device;
+  std::mutex mu;
+  // frame table scratch (indexed + serial modes)
+  void* tab_mem;
+  uint64_t tab_cap;
+  uint64_t* tab_count;
+  uint32_t* err;  // device error word
+  stream_scratch ss;  // fused stream decoder scratch (xyws_stream.hip)
+};
+
+namespace {
+
+struct device_guard {
+  int prev = -1;
+  bool ok = false;
+  explicit device_guard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~device_guard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int hip_err(hipError_t e) { return e == hipSuccess ? XYWS_OK : XYWS_ERR_HIP; }
+
+int ensure_table(xyws_ctx* ctx, uint64_t n) {
+  if (n <= ctx->tab_cap && ctx->tab_mem) return XYWS_OK;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)cs;
+  uint64_t cap = n < 1024 ? 1024 : n;
+  void* mem = nullptr;
+  size_t bytes = cap * (8 + 8 + 8 + 4) + 64;
+  if (hipMalloc(&mem, bytes) != hipSuccess) return XYWS_ERR_NOMEM;
+  if (ctx->tab_mem) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(ctx->tab_mem);
+  }
+  ctx->tab_mem = mem;
+  ctx->tab_cap = cap;
+  return XYWS_OK;
+}
+
+frame_table table_of(xyws_ctx* ctx) {
+  frame_table t;
+  char* m = static_cast<char*>(ctx->tab_mem);
+  t.start = reinterpret_cast<uint64_t*>(m);
+  t.ps = t.start + ctx->tab_cap;
+  t.pe = t.ps + ctx->tab_cap;
+  t.count = t.pe + ctx->tab_cap;
+  t.kw = reinterpret_cast<uint32_t*>(t.count + 8);
+  return t;
+}
+
+int grid_for(uint64_t items, uint32_t per_block, uint32_t cap) {
+  uint64_t g = (items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int xyws_abi_version(void) { return XYWS_ABI_VERSION; }
+
+const char* xyws_strerror(int code) {
+  switch (code) {
+    case XYWS_OK: return "ok";
+    case XYWS_ERR_INVALID: return "invalid argument";
+    case XYWS_ERR_HIP: return "HIP runtime error";
+    case XYWS_ERR_NOMEM: return "device allocation failed";
+    case XYWS_ERR_CAPACITY: return "scratch capacity exceeded";
+    case XYWS_ERR_DEVICE: return "device-side error";
+    default: return "unknown error";
+  }
+}
+
+int xyws_ctx_create(int device, xyws_ctx** out) {
+  if (!out) return XYWS_ERR_INVALID;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return XYWS_ERR_HIP;
+  if (device < 0 || device >= ndev) return XYWS_ERR_INVALID;
+  device_guard g(device);
+  if (!g.ok) return XYWS_ERR_HIP;
+  xyws_ctx* c = new xyws_ctx();
+  c->device = device;
+  c->tab_mem = nullptr;
+  c->tab_cap = 0;
+  c->err = nullptr;
+  stream_scratch_init(&c->ss);
+  if (hipMalloc(&c->err, 64) != hipSuccess) {
+    delete c;
+    return XYWS_ERR_NOMEM;
+  }
+  if (hipMemset(c->err, 0, 64) != hipSuccess) {
+    (void)hipFree(c->err);
+    delete c;
+    return XYWS_ERR_HIP;
+  }
+  *out = c;
+  return XYWS_OK;
+}
+
+int xyws_ctx_destroy(xyws_ctx* ctx) {
+  if (!ctx) return XYWS_ERR_INVALID;
+  {
+    device_guard g(ctx->device);
+    (void)hipDeviceSynchronize();
+    if (ctx->tab_mem) (void)hipFree(ctx->tab_mem);
+    if (ctx->err) (void)hipFree(ctx->err);
+    stream_scratch_free(&ctx->ss);
+  }
+  delete ctx;
+  return XYWS_OK;
+}
+
+int xyws_ctx_reserve(xyws_ctx* ctx, uint64_t max_batch_bytes, uint64_t max_frames) {
+  if (!ctx) return XYWS_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  device_guard g(ctx->device);
+  if (!g.ok) return XYWS_ERR_HIP;
+  int rc = ensure_table(ctx, max_frames);
+  if (rc) return rc;
+  return stream_scratch_reserve(&ctx->ss, max_batch_bytes);
+}
+
+int xyws_ctx_last_device_error(xyws_ctx* ctx, uint32_t* out) {
+  if (!ctx || !out) return XYWS_ERR_INVALID;
+  device_guard g(ctx->device);
+  if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
+  uint32_t v[2] = {0, 0};
+  if (hipMemcpy(v, ctx->err, 4, hipMemcpyDeviceToHost) != hipSuccess) return XYWS_ERR_HIP;
+  *out = v[0] | stream_scratch_error(&ctx->ss);
+  return XYWS_OK;
+}
+
+int xyws_unmask(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4], uint64_t phase,
+                uint64_t* phase_out, void* stream) {
+  if (!ctx || !key || (!dev && len)) return XYWS_ERR_INVALID;
+  if (phase_out) *phase_out = phase + len;
+  if (!len) return XYWS_OK;
+  device_guard g(ctx->device);
+  if (!g.ok) return XYWS_ERR_HIP;
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(dev);
+  uint8_t* base = reinterpret_cast<uint8_t*>(addr & ~(uintptr_t)15);
+  const uint64_t lo = addr & 15, hi = lo + len;
+  const uint32_t k = (uint32_t)key[0] | ((uint32_t)key[1] << 8) | ((uint32_t)key[2] << 16) |
+                     ((uint32_t)key[3] << 24);
+  // aligned_key(k, lo, phase) on the host: rotation by (phase - lo) mod 4
+  const uint32_t c = (uint32_t)(phase - lo) & 3u;
+  const uint32_t kw = c ? ((k >> (8u * c)) | (k << (32u - 8u * c))) : k;
+  const uint64_t chunks = ((hi + 15) >> 4) - (lo >> 4);
+  hipLaunchKernelGGL(k_unmask_range, dim3(grid_for(chunks, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, base, lo, hi, kw);
+  return hip_err(hipGetLastError());
+}
+
+int xyws_decode_indexed(xyws_ctx* ctx, void* dev_buf, uint64_t len, const uint64_t* dev_starts,
+                        uint64_t n, xyws_frame* dev_frames, uint32_t opts, void* stream) {
+  if (!ctx || (!dev_buf && len) || (!dev_starts && n)) return XYWS_ERR_INVALID;
+  if (!n) return XYWS_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  device_guard g(ctx->device);
+  if (!g.ok) return XYWS_ERR_HIP;
+  int rc = ensure_table(ctx, n);
+  if (rc) return rc;
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(dev_buf);
+  uint8_t* base = reinterpret_cast<uint8_t*>(addr & ~(uintptr_t)15);
+  const uint64_t lo = addr & 15, hi = lo + len;
+  frame_table t = table_of(ctx);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_parse_indexed, dim3(grid_for(n, 256, 1u << 30)), dim3(256), 0, s, base, lo, hi,
+                     dev_starts, n, t, dev_frames);
+  if ((rc = hip_err(hipGetLastError()))) return rc;
+  if (!(opts & XYWS_OPT_PARSE_ONLY) && len) {
+    const uint64_t tiles = (hi - (lo & ~(uint64_t)(UNMASK_TILE - 1)) + UNMASK_TILE - 1) / UNMASK_TILE;
+    hipLaunchKernelGGL(k_unmask_tiles, dim3(grid_for(tiles, 1, 4096)), dim3(UNMASK_THREADS), 0, s,
+                       base, lo, hi, t);
+    rc = hip_err(hipGetLastError());
+  }
+  return rc;
+}
+
+int xyws_decode_stream(xyws_ctx* ctx, void* dev_buf, uint64_t len, const xyws_carry* dev_carry_in,
+                       xyws_carry* dev_carry_out, xyws_frame* dev_frames, uint64_t cap,
+                       uint64_t* dev_nframes, uint32_t opts, void* stream) {
+  if (!ctx || (!dev_buf && len)) return XYWS_ERR_INVALID;
+  if (len >= (1ull << 46)) return XYWS_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  device_guard g(ctx->device);
+  if (!g.ok) return XYWS_ERR_HIP;
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(dev_buf);
+  uint8_t* base = reinterpret_cast<uint8_t*>(addr & ~(uintptr_t)15);
+  const uint64_t lo = addr & 15, hi = lo + len;
+  hipStream_t s = (hipStream_t)stream;
+  if ((opts & XYWS_OPT_SERIAL_SCAN) || !XYWS_HAVE_FUSED) {
+    // worst case is a 2-byte unmasked frame every 2 bytes; the debug path caps
+    // its table at 2^24 frames and flags the device error word beyond that.
+    uint64_t want = len / 2 + 2;
+    if (want > (1ull << 24)) want = 1ull << 24;
+    int rc = ensure_table(ctx, want);
+    if (rc) return rc;
+    frame_table t = table_of(ctx);
+    hipLaunchKernelGGL(k_stream_serial, dim3(1), dim3(64), 0, s, base, lo, hi, dev_carry_in,
+                       dev_carry_out, t, ctx->tab_cap, dev_frames, cap, dev_nframes, ctx->err);
+    if ((rc = hip_err(hipGetLastError()))) return rc;
+    if (!(opts & XYWS_OPT_PARSE_ONLY) && len) {
+      const uint64_t tiles = (hi - (lo & ~(uint64_t)(UNMASK_TILE - 1)) + UNMASK_TILE - 1) / UNMASK_TILE;
+      hipLaunchKernelGGL(k_unmask_tiles, dim3(grid_for(tiles, 1, 4096)), dim3(UNMASK_THREADS), 0, s,
+                         base, lo, hi, t);
+      rc = hip_err(hipGetLastError());
+    }
+    return rc;
+  }
+  return stream_decode_fused(&ctx->ss, base, lo, hi, dev_carry_in, dev_carry_out, dev_frames, cap,
+                             dev_nframes, opts, s);
+}
+
+}  // extern "C"

@@ -1,0 +1,319 @@
+"""Host-side mirror of xynet's WebSocket frame interface, backed by the gfx950 path.
+
+Names, argument meaning and error behaviour follow the reference headers
+(paths relative to the xynet tree):
+
+  websocket_flags                  include/xynet/http/websocket_frame_header.h:42-106
+  calc_frame_header_size / _size   :111-131, WS_MAX_FRAME_HEADER_SIZE :134
+  websocket_frame_header           :179-224  (encode side; built on the host, as the
+                                              reference builds reply headers)
+  websocket_frame_header_parser    :226-303  (parse/result/reset/npos over device bytes)
+  websocket_mask                   include/xynet/http/websocket_frame_mask.h:6-25
+  frame_decoder.decode             the batched websocket_recv_data
+                                   (example/include/common/websocket.h:110-134)
+
+Device buffers are torch uint8 tensors on a ROCm device (PyTorch is used only
+for device memory and streams). Every computing call runs HIP kernels from
+libxyws.so through its C-ABI; there is no CPU fallback.
+"""
+import ctypes as C
+import enum
+import threading
+
+from . import _lib
+from ._lib import Carry, Frame, XywsError, check
+
+npos = (1 << 64) - 1
+
+
+class websocket_flags(enum.IntFlag):
+    """enum class websocket_flags (websocket_frame_header.h:42-58)."""
+    WS_NONE = 0x0
+    WS_OP_CONTINUE = 0x0
+    WS_OP_TEXT = 0x1
+    WS_OP_BINARY = 0x2
+    WS_OP_CLOSE = 0x8
+    WS_OP_PING = 0x9
+    WS_OP_PONG = 0xA
+    WS_OP_MASK = 0xF
+    WS_FIN = 0x10
+    WS_FINAL_FRAME = 0x10
+    WS_HAS_MASK = 0x20
+
+
+def websocket_flags_not_none(flag):
+    """websocket_flags_not_none (:61-64)."""
+    return bool(int(flag))
+
+
+def calc_frame_header_size(flags, data_len):
+    """detail::calc_frame_header_size (:111-126)."""
+    size = 2
+    if data_len >= 126:
+        size += 8 if data_len > 0xFFFF else 2
+    if int(flags) & websocket_flags.WS_HAS_MASK:
+        size += 4
+    return size
+
+
+def calc_frame_size(flags, data_len):
+    """detail::calc_frame_size (:128-131)."""
+    return data_len + calc_frame_header_size(flags, data_len)
+
+
+WS_MAX_FRAME_HEADER_SIZE = calc_frame_header_size(websocket_flags.WS_HAS_MASK, 0xFFFFFFFF)
+
+
+def _builder(flags, mask, data_len):
+    """detail::websocket_frame_header_builder (:136-175): returns the header bytes;
+    key bytes are written only when `mask` is given (:168-171)."""
+    flags = int(flags)
+    b0 = (0x80 if flags & websocket_flags.WS_FIN else 0) | (flags & 0x0F)
+    b1 = 0x80 if flags & websocket_flags.WS_HAS_MASK else 0
+    if data_len < 126:
+        out = bytearray([b0, b1 | data_len])
+    elif data_len <= 0xFFFF:
+        out = bytearray([b0, b1 | 126]) + data_len.to_bytes(2, "big")
+    else:
+        out = bytearray([b0, b1 | 127]) + (data_len & ((1 << 64) - 1)).to_bytes(8, "big")
+    if flags & websocket_flags.WS_HAS_MASK:
+        out += bytes(mask) if mask is not None else b"\0\0\0\0"
+    return bytes(out)
+
+
+class websocket_frame_header:
+    """class websocket_frame_header (:179-224).
+
+    Reference behaviour is kept in parity mode: the masked constructors store
+    the key beside the header and build the header WITHOUT it (:186-188,
+    :191-202), so the key bytes on the wire are zero. ``with_key`` builds the
+    RFC-correct masked header (client role) instead.
+    """
+
+    def __init__(self, flags, data_len, mask=None):
+        self._mask = b"\0\0\0\0"
+        if mask is not None:
+            self._mask = (mask.to_bytes(4, "little") if isinstance(mask, int) else bytes(mask))
+        self._header = _builder(flags, None, data_len)
+
+    @classmethod
+    def with_key(cls, flags, data_len, key):
+        h = cls(flags, data_len)
+        key = key.to_bytes(4, "little") if isinstance(key, int) else bytes(key)
+        h._mask = key
+        h._header = _builder(int(flags) | websocket_flags.WS_HAS_MASK, key, data_len)
+        return h
+
+    def view(self):
+        return self._header
+
+    def span(self):
+        return self._header
+
+    def __len__(self):
+        return len(self._header)
+
+
+# ---------------------------------------------------------------------------
+# device plumbing
+
+class Context:
+    """An xyws_ctx bound to one HIP device (one per thread and device)."""
+
+    def __init__(self, device=0):
+        self.L = _lib.load()
+        self.device = device
+        h = C.c_void_p()
+        check(self.L.xyws_ctx_create(device, C.byref(h)), "xyws_ctx_create")
+        self.h = h
+
+    def reserve(self, max_batch_bytes, max_frames=0):
+        check(self.L.xyws_ctx_reserve(self.h, max_batch_bytes, max_frames), "xyws_ctx_reserve")
+
+    def last_device_error(self):
+        v = C.c_uint32()
+        check(self.L.xyws_ctx_last_device_error(self.h, C.byref(v)))
+        return v.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.xyws_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_tls = threading.local()
+
+
+def context(device=None):
+    import torch
+    dev = torch.cuda.current_device() if device is None else int(device)
+    cache = getattr(_tls, "ctx", None)
+    if cache is None:
+        cache = _tls.ctx = {}
+    if dev not in cache:
+        cache[dev] = Context(dev)
+    return cache[dev]
+
+
+def _dev_u8(t):
+    import torch
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise XywsError(-1, "expected a device-resident torch tensor")
+    if t.dtype != torch.uint8 or not t.is_contiguous():
+        raise XywsError(-1, "expected a contiguous uint8 tensor")
+    return t
+
+
+def _stream(t):
+    import torch
+    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def websocket_mask(data, mask, i=0):
+    """websocket_mask(R&& data, uint32_t mask, size_t i) -> size_t
+    (websocket_frame_mask.h:6-25) on a device tensor: in place,
+    data[j] ^= bytes(mask)[(i + j) % 4]; returns i + len(data)."""
+    t = _dev_u8(data)
+    ctx = context(t.device.index)
+    key = (C.c_uint8 * 4)(*int(mask & 0xFFFFFFFF).to_bytes(4, "little"))
+    out = C.c_uint64()
+    check(ctx.L.xyws_unmask(ctx.h, C.c_void_p(t.data_ptr()), t.numel(), key, int(i),
+                            C.byref(out), _stream(t)), "xyws_unmask")
+    return out.value
+
+
+def _frames_from_device(frames_t, n):
+    import numpy as np
+    raw = frames_t[: n * 32].cpu().numpy().tobytes() if n else b""
+    arr = (Frame * max(n, 1)).from_buffer_copy(raw.ljust(max(n, 1) * 32, b"\0"))
+    return [arr[k] for k in range(n)], np
+
+
+class DecodeResult:
+    """Frames and count of one decode call (device tensors; host copies on demand)."""
+
+    def __init__(self, frames_t, nframes_t, cap):
+        self.frames_t = frames_t
+        self.nframes_t = nframes_t
+        self.cap = cap
+
+    @property
+    def nframes(self):
+        return int(self.nframes_t.item()) if self.nframes_t is not None else None
+
+    def frames(self):
+        if self.frames_t is None:
+            return []
+        n = min(self.nframes, self.cap)
+        return _frames_from_device(self.frames_t, n)[0]
+
+
+class frame_decoder:
+    """Batched, device-resident websocket_recv_data: parse every frame of
+    back-to-back batches and unmask payloads in place, carrying a frame or header
+    cut by a batch end into the next batch (xyws_decode_stream)."""
+
+    def __init__(self, device=None, serial=False, parse_only=False):
+        import torch
+        self.ctx = context(device)
+        self.device = torch.device("cuda", self.ctx.device)
+        self.carry_t = torch.zeros(64, dtype=torch.uint8, device=self.device)
+        self.opts = (4 if serial else 0) | (1 if parse_only else 0)
+
+    def reset(self):
+        self.carry_t.zero_()
+
+    def carry(self):
+        return Carry.from_buffer_copy(self.carry_t.cpu().numpy().tobytes())
+
+    def decode(self, buf, cap=0, count=True, carry=True):
+        """Decode one batch in place. cap: frame descriptors to return; count:
+        return the frame count; carry=False decodes the batch as a fresh stream
+        and keeps no state (no carry read or written)."""
+        import torch
+        t = _dev_u8(buf)
+        frames_t = torch.empty(max(cap, 1) * 32, dtype=torch.uint8, device=self.device) if cap else None
+        n_t = torch.zeros(1, dtype=torch.int64, device=self.device) if count else None
+        cp = C.c_void_p(self.carry_t.data_ptr()) if carry else None
+        check(self.ctx.L.xyws_decode_stream(
+            self.ctx.h, C.c_void_p(t.data_ptr()), t.numel(), cp, cp,
+            C.c_void_p(frames_t.data_ptr()) if frames_t is not None else None, cap,
+            C.c_void_p(n_t.data_ptr()) if n_t is not None else None, self.opts, _stream(t)),
+            "xyws_decode_stream")
+        return DecodeResult(frames_t, n_t, cap)
+
+
+def decode_indexed(buf, starts, frames=True, parse_only=False):
+    """Frames at known offsets (ascending): parse + unmask in place."""
+    import torch
+    t = _dev_u8(buf)
+    ctx = context(t.device.index)
+    st = torch.as_tensor(starts, dtype=torch.int64).to(t.device)
+    n = st.numel()
+    frames_t = torch.empty(max(n, 1) * 32, dtype=torch.uint8, device=t.device) if frames else None
+    check(ctx.L.xyws_decode_indexed(
+        ctx.h, C.c_void_p(t.data_ptr()), t.numel(), C.c_void_p(st.data_ptr()), n,
+        C.c_void_p(frames_t.data_ptr()) if frames_t is not None else None,
+        1 if parse_only else 0, _stream(t)), "xyws_decode_indexed")
+    res = DecodeResult(frames_t, None, n)
+    res.nframes_t = torch.tensor([n], dtype=torch.int64)
+    return res
+
+
+class websocket_frame_header_parser:
+    """websocket_frame_header_parser (:226-303) over device-resident bytes.
+
+    parse(bytes) returns the number of bytes consumed in THIS call up to the
+    end of the header, or ``npos`` while the header is incomplete; once a header
+    completed, further input returns npos until reset() (:305-385). result()
+    returns (flags, mask_uint32_t, length) after a completed header (the
+    reference's usage, websocket.h:121-128). Each call runs the device decoder
+    in parse-only mode; state lives in a device-side xyws_carry.
+    """
+    npos = npos
+
+    def __init__(self, device=None):
+        self._dec = frame_decoder(device, parse_only=True)
+        self._finished = False
+        self._res = (websocket_flags.WS_NONE, 0, 0)
+
+    def reset(self):
+        self._dec.reset()
+        self._finished = False
+        self._res = (websocket_flags.WS_NONE, 0, 0)
+
+    def parse(self, data):
+        if self._finished:
+            return npos
+        t = _dev_u8(data)
+        if t.numel() == 0:
+            return npos
+        before = self._dec.carry().hdr_len
+        r = self._dec.decode(t, cap=1)
+        if r.nframes == 0:
+            return npos
+        f = r.frames()[0]
+        self._finished = True
+        self._res = (websocket_flags(f.flags), int.from_bytes(bytes(f.key), "little"), f.payload_len)
+        return f.hdr_len - before
+
+    def flags(self):
+        return self._res[0]
+
+    def length(self):
+        return self._res[2]
+
+    def mask_uint32_t(self):
+        return self._res[1]
+
+    def mask(self):
+        return self._res[1].to_bytes(4, "little")
+
+    def result(self):
+        return self._res
