@@ -284,9 +284,10 @@ void oracle_decode_indexed(uint8_t* buf, uint64_t len, const uint64_t* starts, u
       f.status = oracle_header_status(buf + s, plen);
       uint64_t lim = len;
       if (i + 1 < n && starts[i + 1] < lim) lim = starts[i + 1];
+      uint64_t end = (plen > UINT64_MAX - ps) ? UINT64_MAX : ps + plen; /* saturating */
       uint64_t pe = (plen > len - ps) ? len : ps + plen;
-      if (pe > len || plen > len - ps) f.status |= XYWS_ST_PAYLOAD_INCOMPLETE;
-      if (i + 1 < n && pe > starts[i + 1]) f.status |= XYWS_ST_OVERLAP;
+      if (plen > len - ps) f.status |= XYWS_ST_PAYLOAD_INCOMPLETE;
+      if (i + 1 < n && end > starts[i + 1]) f.status |= XYWS_ST_OVERLAP;
       if (pe > lim) pe = lim;
       if (pe > ps) oracle_mask(buf + ps, pe - ps, oracle_parser_mask_u32(&p), 0);
     }

@@ -98,11 +98,10 @@ __global__ void __launch_bounds__(256) k_parse_indexed(const uint8_t* __restrict
     pe = end < hi ? end : hi;
     uint8_t st = h.status;
     if (end > hi) st |= XYWS_ST_PAYLOAD_INCOMPLETE;
-    if (i + 1 < n) {
-      uint64_t nx_rel = starts[i + 1];
-      uint64_t nx = lo + (nx_rel < len ? nx_rel : len);
-      if (end > nx) st |= XYWS_ST_OVERLAP;
-      if (pe > nx) pe = nx;
+    if (i + 1 < n) {  // clip at the next caller start (relative coordinates: no overflow)
+      const uint64_t nx_rel = starts[i + 1];
+      if (end - lo > nx_rel) st |= XYWS_ST_OVERLAP;
+      if (nx_rel < len && pe > lo + nx_rel) pe = lo + nx_rel;
     }
     if (pe < ps) pe = ps;
     f.payload_off = (int64_t)(s_rel + h.hlen);
