@@ -187,6 +187,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--host-path", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--stats", action="store_true", help="print fused-decoder resolution counters")
     args = ap.parse_args()
 
     import torch
@@ -235,6 +236,17 @@ def main():
         elapsed = float(t.item())
     kernel_ms = sorted(a.elapsed_time(b) for a, b in evs)
     avg_ms = sum(kernel_ms) / len(kernel_ms)
+
+    if args.stats and rank == 0:  # one extra counted decode pair (keeps the step parity)
+        names = ["lookbacks", "lb_windows", "lb_segments", "lb_stalls", "lb_wait_incl",
+                 "help_windows", "help_segments", "mode1", "mode2", "survivors", "spins"]
+        for _ in range(2):
+            dec.opts |= 0x100
+            dec.decode(buf, cap=0, count=False, carry=False)
+            dec.opts &= ~0x100
+            out = (C.c_uint64 * 16)()
+            dec.ctx.L.xyws_debug_stats(dec.ctx.h, out)
+        print(json.dumps({"stats": dict(zip(names, list(out)[:len(names)]))}), flush=True)
 
     # parity after the timed region: total decodes = warmup + steps
     dev_err = dec.ctx.last_device_error()

@@ -23,7 +23,7 @@ for step in "$@"; do
     tests_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
-    bench_quick) run bench_quick 300 python bench.py --steps 10 --warmup 2 --no-cpu ;;
+    bench_quick) run bench_quick 300 python bench.py --steps 10 --warmup 2 --no-cpu --stats ;;
     bench_c2) run bench_c2 300 python bench.py --config c2 --no-cpu ;;
     bench_c1) run bench_c1 300 python bench.py --config c1 --no-cpu ;;
     bench_c4) run bench_c4 300 python bench.py --config c4 --no-cpu ;;

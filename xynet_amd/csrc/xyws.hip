@@ -26,7 +26,7 @@
 #include "xyws_stream.h"
 
 #ifndef XYWS_HAVE_FUSED
-#define XYWS_HAVE_FUSED 0
+#define XYWS_HAVE_FUSED 1
 #endif
 
 // ---------------------------------------------------------------------------
@@ -411,6 +411,14 @@ int xyws_ctx_last_device_error(xyws_ctx* ctx, uint32_t* out) {
   if (hipMemcpy(v, ctx->err, 4, hipMemcpyDeviceToHost) != hipSuccess) return XYWS_ERR_HIP;
   *out = v[0] | stream_scratch_error(&ctx->ss);
   return XYWS_OK;
+}
+
+// Internal (not part of include/xyws.h): resolution counters of the last fused
+// stream decode run with XYWS_OPT_STATS (0x100). Synchronizes the device.
+int xyws_debug_stats(xyws_ctx* ctx, uint64_t out[16]) {
+  if (!ctx || !out) return XYWS_ERR_INVALID;
+  device_guard g(ctx->device);
+  return stream_scratch_stats(&ctx->ss, out);
 }
 
 int xyws_unmask(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4], uint64_t phase,

@@ -15,7 +15,11 @@ struct stream_scratch {
 void stream_scratch_init(stream_scratch* s);
 void stream_scratch_free(stream_scratch* s);
 int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes);
-uint32_t stream_scratch_error(stream_scratch* s);  // synchronous read of the error word
+uint32_t stream_scratch_error(stream_scratch* s);
+int stream_scratch_stats(stream_scratch* s, uint64_t out[16]);
+
+// Internal decode option: count resolution events (xyws_debug_stats).
+#define XYWS_OPT_STATS 0x100u  // synchronous read of the error word
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
                         const xyws_carry* cin, xyws_carry* cout, xyws_frame* frames, uint64_t cap,
                         uint64_t* nframes, uint32_t opts, hipStream_t stream);

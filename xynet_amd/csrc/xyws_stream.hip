@@ -1,11 +1,1187 @@
-// xyws_stream.hip — fused single-pass stream decoder (placeholder: not yet built).
-#include "xyws_stream.h"
+// xyws_stream.hip — fused single-pass stream decoder for gfx950 (default mode of
+// xyws_decode_stream).
+//
+// Problem: in a back-to-back batch the start of frame k+1 is known only after
+// the header of frame k is parsed (websocket_frame_header.h:305-385 gives the
+// header size and the payload length), so frame boundaries form a linked list
+// through the batch. A serial chase from HBM costs one dependent load per
+// frame; a separate index pass would read the batch twice. This kernel reads
+// every byte once and keeps it in registers until its frames are known.
+//
+// Geometry: a SEGMENT is 64 KiB owned by one 256-thread workgroup; lane t
+// holds 16 chunks of 16 B (chunk k at segment offset (k*256 + t)*16, so each
+// load instruction of a wave covers 1 KiB contiguously) = 64 VGPRs, loaded and
+// stored through a per-segment buffer descriptor (base and range in SGPRs, one
+// 32-bit offset per lane). Two workgroups fit per CU (VGPRs <= 256, LDS ~62
+// KiB each): while one resolves boundaries the other streams. (128 KiB
+// segments, 128 data VGPRs, spilled: the resolution code needs the rest.) Segments are handed out by an atomic ticket,
+// so every segment a workgroup waits on is owned by a running workgroup
+// (forward progress with no co-residency assumption).
+//
+// Per segment:
+//  1. Issue all 16 loads. For each 32 KiB sub-tile: copy it (+16 B halo) to
+//     LDS, SWAR-prefilter every byte position for a plausible client header
+//     (RSV = 0, known opcode, MASK set), fully parse the candidates (minimal
+//     length form, control-frame rules, frame fits the batch, successor inside
+//     the sub-tile is itself a candidate) and append the survivors, in
+//     position order, to a segment-wide survivor list.
+//  2. Link survivors (successor = survivor at pos + H + len, or EXIT past the
+//     segment) and walk the graph once (memoized): every node learns its
+//     outcome (which exit it reaches), its remaining frame count, and — on the
+//     first walk that reached each outcome — its ordinal along that walk.
+//     Speculation over a 64 KiB span is strong: a false candidate must chain
+//     through plausible headers all the way out of the segment.
+//  3. Publish the AGGREGATE record: the first 8 exiting nodes (position,
+//     outcome, remaining count) and up to 4 outcomes (exit, last frame).
+//  4. Decoupled look-back: the nearest INCLUSIVE predecessor gives an exact
+//     state; it is carried through later segments with their aggregates (the
+//     exact entry must be one of their published nodes, or lie past them), or
+//     we wait for that segment's own inclusive record. After resolving its own
+//     segment a workgroup keeps HELPING: it carries the exact state forward
+//     through successors whose aggregates are already published and publishes
+//     their inclusive records, so the frontier runs ahead of the data.
+//  5. The exact in-segment chain from the true entry: the suffix of a primary
+//     walk (parallel, by ordinal) or an exact header chase in global memory
+//     (header bytes are never modified, so any workgroup may read them).
+//  6. XOR every register chunk with the rotated keys of the frames covering it
+//     and store the changed chunks.
+// Speculation only decides speed; correctness rests on the exact state of
+// step 4 and the exact chain of step 5, so any byte stream (RSV bits, reserved
+// opcodes, unmasked or non-minimal frames) decodes as the reference parses it.
+//
+// Inter-workgroup hand-off follows MI355X_MICROARCH.md §Workgroup dispatch
+// (table row 1): record words are written with agent-scope (sc1) stores by ONE
+// lane, drained with s_waitcnt vmcnt(0), then an sc1 flag store; readers poll
+// the flag with sc1 loads and read the record with sc1 loads. Flags and the
+// ticket are zeroed by hipMemsetAsync before every launch. Every spin is
+// bounded and reports through the device error word.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
 
-void stream_scratch_init(stream_scratch* s) { s->mem = nullptr; s->bytes = 0; s->max_tiles = 0; }
-void stream_scratch_free(stream_scratch* s) { if (s->mem) (void)hipFree(s->mem); s->mem = nullptr; }
-int stream_scratch_reserve(stream_scratch*, uint64_t) { return XYWS_OK; }
-uint32_t stream_scratch_error(stream_scratch*) { return 0; }
-int stream_decode_fused(stream_scratch*, uint8_t*, uint64_t, uint64_t, const xyws_carry*, xyws_carry*,
-                        xyws_frame*, uint64_t, uint64_t*, uint32_t, hipStream_t) {
-  return XYWS_ERR_INVALID;
+#include "xyws_stream.h"
+#include "xyws_device.h"
+
+namespace {
+
+constexpr uint32_t SEG = 65536;          // segment bytes (per workgroup)
+constexpr uint32_t SUB = 32768;          // sub-tile bytes staged in LDS
+constexpr uint32_t NSUB = SEG / SUB;     // 2
+constexpr uint32_t NT = 256;             // threads per workgroup
+constexpr uint32_t CHS = SEG / (16 * NT);  // 32 chunks per lane
+constexpr uint32_t CHSUB = SUB / (16 * NT);  // 8 chunks per lane per sub-tile
+constexpr uint32_t HALO = 16;
+constexpr uint32_t SMAX = 1024;          // survivors tracked per segment
+constexpr uint32_t FCAP = SUB / 16;      // frame-list entries per pass (overlays the sub-tile)
+constexpr uint32_t NENT = 16;            // aggregate entry nodes (2 per record word)
+constexpr uint32_t NOUT = 8;             // aggregate outcomes (2 record words each)
+constexpr uint32_t HELP = 128;           // segments helped forward per resolution
+constexpr uint32_t SPIN = 1u << 24;      // bounded spins (~1 s)
+
+constexpr uint32_t F_AGG = 1, F_INCL = 2;
+constexpr uint16_t N_EXIT = 0xFFFF, N_DEAD = 0xFFFE;
+constexpr uint8_t O_NONE = 0xFF, O_DEAD = 0xFE, O_UNREC = 0xFD;  // node outcome marks
+constexpr uint16_t ORD_NONE = 0xFFFF;
+
+// composition-state bits
+constexpr uint32_t S_PARTIAL = 1;    // stream ended in an incomplete header at X
+constexpr uint32_t S_NOCOV = 2;      // no frame covers the bytes before X
+constexpr uint32_t S_CARRIED = 4;    // covering frame = the open frame carried in
+constexpr uint32_t S_HDRCARRY = 8;   // covering frame's header began in the previous batch
+constexpr uint32_t S_PARTCARRY = 16; // the carried partial header is still incomplete
+constexpr uint32_t S_KEEP = S_NOCOV | S_CARRIED | S_HDRCARRY;
+
+// record layout: 64 x u64 per segment
+enum {
+  R_META = 0,              // n_entries | n_outcomes << 8 | overflow << 16
+  R_ENT0 = 1,              // NENT entries, two per word: pos (16) | rem (13) << 16 | outcome (3) << 29
+  R_OUT0 = 9,              // NOUT outcomes x 2 words: exit; cov_ps - ss (20) | hlen (4) << 20 | kw << 32
+  R_INC = 32,              // X, cov_ps, cov_start, kw | st << 32, cnt
+  R_WORDS = 64
+};
+
+struct fent {
+  uint32_t start, ps, end, kw;  // segment-relative; ps/end clamped to [0, 2^32-1]
+};
+
+struct cstate {
+  uint64_t X;          // first frame start >= current position (absolute)
+  uint64_t cov_ps;     // payload start of the frame ending at X
+  uint64_t cov_start;  // header start of that frame
+  uint64_t cnt;        // frames whose header completed before X
+  uint32_t cov_kw;     // aligned key word of that frame
+  uint32_t st;         // S_* bits
+};
+
+struct __attribute__((aligned(16))) st_lds {
+  union {
+    uint8_t sub[SUB + HALO];  // pass 1: sub-tile bytes
+    fent flist[FCAP];         // pass 2: frame list
+  };
+  uint64_t bits[SUB / 64];    // candidate bitmap of the current sub-tile
+  uint32_t s_pos[SMAX];       // survivor position (segment-relative)
+  uint32_t s_nrel[SMAX];      // successor position (segment-relative, saturating)
+  uint32_t s_key[SMAX];
+  uint16_t s_nxt[SMAX];       // successor survivor index / N_EXIT / N_DEAD
+  uint16_t s_rem[SMAX];       // frames from this node to the exit
+  uint16_t s_ord[SMAX];       // ordinal on the primary walk of its outcome
+  uint8_t s_out[SMAX];        // outcome id / O_* mark
+  uint8_t s_hlen[SMAX];
+  uint32_t scan[8];
+  // broadcast scalars
+  uint64_t seg_id;
+  uint32_t nsurv, overflow, nfl, pass_done;
+  cstate in, out;
+  uint64_t chase_X, fbase;
+  uint32_t mode, ord_x, out_x, npre;
+  uint16_t s_ord_pre[64];     // non-primary prefix of the entry's path
+  uint64_t outs[NOUT][4];     // aggregate outcomes: exit, cov_ps, cov_start, kw
+  uint32_t ents[NENT];        // aggregate entries (packed as in the record)
+};
+
+struct st_params {
+  uint8_t* base;
+  uint64_t lo, hi, nseg;
+  const xyws_carry* cin;  // private snapshot of the incoming carry
+  xyws_carry* cout;
+  xyws_frame* frames;
+  uint64_t cap;
+  uint64_t* nframes;
+  uint32_t* head;   // [0] ticket, [1] error word
+  uint32_t* flags;  // one per segment
+  uint64_t* recs;   // R_WORDS per segment
+  uint32_t opts;
+};
+
+// ---------------------------------------------------------------- debug counters
+// With XYWS_OPT_STATS the kernel counts resolution events into head[16..32)
+// (read back by xyws_debug_stats). Off by default: one uniform branch each.
+enum { ST_LB = 0, ST_LB_WIN, ST_LB_SEG, ST_LB_STALL, ST_LB_WAITINC, ST_HELP_WIN, ST_HELP_SEG,
+       ST_MODE1, ST_MODE2, ST_NSURV, ST_SPINS, ST_NSTAT = 16 };
+
+// ---------------------------------------------------------------- hand-off
+XYWS_DEV void st_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+XYWS_DEV uint64_t st_load(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+XYWS_DEV uint32_t flag_load(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+XYWS_DEV void flag_publish(uint32_t* p, uint32_t v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // record stores drained before the flag
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+XYWS_DEV bool stat_on(const st_params& P) { return (P.opts & XYWS_OPT_STATS) != 0; }
+XYWS_DEV void stat_add(const st_params& P, uint32_t i, uint64_t v) {
+  if (__builtin_amdgcn_mbcnt_lo(~0u, 0) == 0)  // one lane
+    atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + i, (unsigned long long)v);
+}
+
+XYWS_DEV bool flag_wait(const uint32_t* p, uint32_t want, uint32_t* err) {
+  for (uint32_t it = 0; it < SPIN; it++) {
+    if (flag_load(p) >= want) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  atomicOr(err, 2u);
+  return false;
+}
+
+// ---------------------------------------------------------------- parsing
+// Header at absolute position p from global memory (header bytes are never
+// written by this kernel). With a carried partial header (h0 > 0) the first h0
+// bytes come from `pre`.
+// Header from 16 little-endian bytes held in four dwords w[0..3] (byte i =
+// w[i/4] >> 8*(i%4)), of which `avail` are valid. Same semantics as
+// parse_header_bytes (websocket_frame_header.h:305-385).
+XYWS_DEV hdr_info parse_header_words(const uint32_t w[4], uint32_t avail) {
+  hdr_info h;
+  h.plen = 0; h.key = 0; h.hlen = 0; h.flags = 0; h.status = 0;
+  if (avail < 2) return h;
+  const uint32_t b0 = w[0] & 0xFF, b1 = (w[0] >> 8) & 0xFF;
+  const uint32_t l7 = b1 & 0x7Fu;
+  const uint32_t ext = l7 == 126 ? 2u : (l7 == 127 ? 8u : 0u);
+  const uint32_t masked = b1 >> 7;
+  const uint32_t need = 2u + ext + 4u * masked;
+  if (avail < need) return h;
+  // bytes 2..9 as a big-endian length; bytes k..k+3 as the key (k = 2 + ext)
+  const uint64_t lo8 = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  const uint64_t hi8 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  const uint64_t b2_9 = (lo8 >> 16) | (hi8 << 48);  // bytes 2..9, little-endian
+  uint64_t len = l7;
+  if (ext == 2) len = ((b2_9 & 0xFF) << 8) | ((b2_9 >> 8) & 0xFF);
+  else if (ext == 8) len = __builtin_bswap64(b2_9);
+  uint32_t key = 0;
+  if (masked) {
+    const uint32_t k = 2 + ext;  // 2, 4 or 10
+    key = (k == 2) ? __builtin_amdgcn_alignbyte(w[1], w[0], 2)
+        : (k == 4) ? w[1] : __builtin_amdgcn_alignbyte(w[3], w[2], 2);
+  }
+  const uint32_t op = b0 & 0x0Fu;
+  uint8_t st = 0;
+  if (b0 & 0x70u) st |= XYWS_ST_RSV;
+  if ((op >= 3 && op <= 7) || op >= 11) st |= XYWS_ST_RESERVED_OPCODE;
+  if ((l7 == 126 && len < 126) || (l7 == 127 && len <= 0xFFFFull)) st |= XYWS_ST_NONMINIMAL_LENGTH;
+  if (l7 == 127 && (len >> 63)) st |= XYWS_ST_LENGTH_MSB;
+  if (op >= 8 && (!(b0 & 0x80u) || len > 125)) st |= XYWS_ST_BAD_CONTROL;
+  if (!masked) st |= XYWS_ST_UNMASKED;
+  h.plen = len;
+  h.key = key;
+  h.hlen = need;
+  h.flags = (uint8_t)(op | ((b0 & 0x80u) ? XYWS_FLAG_FIN : 0u) | (masked ? XYWS_FLAG_HAS_MASK : 0u));
+  h.status = st;
+  return h;
+}
+
+// Four dwords starting at byte address p (any alignment): aligned dword loads
+// (never one that starts at or beyond `limit`) + byte-align funnel shifts.
+XYWS_DEV void load16_global(const uint8_t* base, uint64_t p, uint64_t limit, uint32_t w[4]) {
+  const uint64_t a = p & ~3ull;
+  const uint32_t sh = (uint32_t)(p & 3);
+  uint32_t r[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++)
+    r[i] = (a + 4 * i < limit) ? *reinterpret_cast<const uint32_t*>(base + a + 4 * i) : 0u;
+#pragma unroll
+  for (int i = 0; i < 4; i++) w[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
+}
+
+XYWS_DEV hdr_info header_global(const uint8_t* base, uint64_t p, uint64_t hi) {
+  uint32_t w[4];
+  load16_global(base, p, hi, w);
+  const uint64_t room = hi > p ? hi - p : 0;
+  return parse_header_words(w, room < 16 ? (uint32_t)room : 16u);
+}
+
+// Header whose first h0 bytes were carried from the previous batch.
+XYWS_DEV hdr_info header_carried(const uint8_t* base, uint64_t lo, uint64_t hi, const xyws_carry* c) {
+  uint8_t hb[XYWS_MAX_FRAME_HEADER_SIZE];
+  const uint32_t h0 = c->hdr_len < XYWS_MAX_FRAME_HEADER_SIZE ? c->hdr_len : XYWS_MAX_FRAME_HEADER_SIZE;
+  uint32_t n = 0;
+  for (; n < h0; n++) hb[n] = c->hdr[n];
+  for (; n < XYWS_MAX_FRAME_HEADER_SIZE && lo + (n - h0) < hi; n++) hb[n] = base[lo + (n - h0)];
+  return parse_header_bytes(hb, n);
+}
+
+XYWS_DEV hdr_info header_lds(const uint8_t* sub, uint32_t prel, uint64_t pabs, uint64_t hi) {
+  const uint32_t a = prel & ~3u, sh = prel & 3u;
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(sub + a);
+  uint32_t w[4];
+  const uint32_t r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+  w[0] = __builtin_amdgcn_alignbyte(r1, r0, sh);
+  w[1] = __builtin_amdgcn_alignbyte(r2, r1, sh);
+  w[2] = __builtin_amdgcn_alignbyte(r3, r2, sh);
+  w[3] = __builtin_amdgcn_alignbyte(r4, r3, sh);
+  const uint64_t room = hi > pabs ? hi - pabs : 0;
+  return parse_header_words(w, room < 16 ? (uint32_t)room : 16u);
+}
+
+// Conformance filter of a fully parsed header (speculation only).
+XYWS_DEV bool plausible(const hdr_info& h, uint8_t b1) {
+  if (!h.hlen) return false;
+  const uint32_t op = h.flags & 0x0F;
+  if (op >= 8 && (!(h.flags & XYWS_FLAG_FIN) || h.plen > 125)) return false;
+  const uint32_t l7 = b1 & 0x7F;
+  if (l7 == 126 && h.plen < 126) return false;
+  if (l7 == 127 && (h.plen <= 0xFFFF || (h.plen >> 62))) return false;
+  return true;
+}
+
+XYWS_DEV uint32_t clamp_rel(uint64_t x, uint64_t ts) {
+  if (x <= ts) return 0;
+  const uint64_t d = x - ts;
+  return d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+}
+
+// State before the first byte of the batch (the "inclusive record of segment
+// -1"), from the carry snapshot.
+XYWS_DEV cstate initial_state(const st_params& P) {
+  cstate s;
+  s.X = P.lo; s.cov_ps = P.lo; s.cov_start = P.lo; s.cnt = 0; s.cov_kw = 0; s.st = S_NOCOV;
+  const xyws_carry* c = P.cin;
+  const uint64_t R = c->payload_remaining;
+  if (R) {
+    const uint32_t k = (uint32_t)c->key[0] | ((uint32_t)c->key[1] << 8) |
+                       ((uint32_t)c->key[2] << 16) | ((uint32_t)c->key[3] << 24);
+    s.X = sat_add(P.lo, R);
+    s.cov_ps = P.lo;
+    s.cov_kw = aligned_key(k, P.lo, c->phase);
+    s.st = S_CARRIED;
+    return s;
+  }
+  const uint32_t h0 = c->hdr_len;
+  if (h0) {
+    hdr_info h = header_carried(P.base, P.lo, P.hi, c);
+    if (!h.hlen) {  // still incomplete: the whole batch belongs to the header
+      s.st = S_NOCOV | S_PARTIAL | S_PARTCARRY;
+      return s;
+    }
+    s.cov_start = P.lo;
+    s.cov_ps = P.lo + (h.hlen - h0);
+    s.X = sat_add(s.cov_ps, h.plen);
+    s.cov_kw = aligned_key(h.key, s.cov_ps, 0);
+    s.cnt = 1;
+    s.st = S_HDRCARRY;
+  }
+  return s;
+}
+
+XYWS_DEV cstate rec_incl(const uint64_t* r) {
+  cstate s;
+  uint64_t w[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++) w[i] = st_load(r + R_INC + i);
+  s.X = w[0]; s.cov_ps = w[1]; s.cov_start = w[2];
+  s.cov_kw = (uint32_t)w[3]; s.st = (uint32_t)(w[3] >> 32); s.cnt = w[4];
+  return s;
+}
+
+XYWS_DEV void pub_incl(const st_params& P, uint64_t seg, const cstate& s) {
+  uint64_t* r = P.recs + seg * R_WORDS;
+  st_store(r + R_INC + 0, s.X);
+  st_store(r + R_INC + 1, s.cov_ps);
+  st_store(r + R_INC + 2, s.cov_start);
+  st_store(r + R_INC + 3, (uint64_t)s.cov_kw | ((uint64_t)s.st << 32));
+  st_store(r + R_INC + 4, s.cnt);
+  flag_publish(P.flags + seg, F_INCL);
+}
+
+// Exact chase by header reads in global memory from s.X while s.X < lim.
+XYWS_DEV void chase_global(const st_params& P, cstate& s, uint64_t lim, uint32_t max_hops,
+                           bool* incomplete) {
+  const uint64_t stop = lim < P.hi ? lim : P.hi;
+  for (uint32_t hop = 0; hop < max_hops; hop++) {
+    if ((s.st & S_PARTIAL) || s.X >= stop) return;
+    hdr_info h = header_global(P.base, s.X, P.hi);
+    if (!h.hlen) { s.st = (s.st & S_KEEP) | S_PARTIAL; return; }
+    s.cov_start = s.X;
+    s.cov_ps = s.X + h.hlen;
+    s.cov_kw = aligned_key(h.key, s.cov_ps, 0);
+    s.X = sat_add(s.cov_ps, h.plen);
+    s.cnt++;
+    s.st = 0;
+  }
+  if (!(s.st & S_PARTIAL) && s.X < stop) *incomplete = true;
+}
+
+// ---------------------------------------------------------------- wave-level look-back
+XYWS_DEV uint32_t rl32(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+XYWS_DEV uint64_t rl64(uint64_t v, uint32_t l) {
+  return ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32) | rl32((uint32_t)v, l);
+}
+XYWS_DEV cstate bcast_state(const cstate& s) {  // lane 0's state to every lane
+  cstate r;
+  r.X = rl64(s.X, 0); r.cov_ps = rl64(s.cov_ps, 0); r.cov_start = rl64(s.cov_start, 0);
+  r.cnt = rl64(s.cnt, 0); r.cov_kw = rl32(s.cov_kw, 0); r.st = rl32(s.st, 0);
+  return r;
+}
+
+// One lane's view of segment i's status and records (sc1 loads).
+struct seg_view {
+  uint32_t f;              // flag
+  uint32_t meta;
+  uint64_t ent[NENT / 2];  // packed entry pairs
+  uint64_t out[NOUT][2];   // packed outcomes
+  uint64_t inc[5];
+};
+
+XYWS_DEV void load_view(const st_params& P, uint64_t i, bool valid, seg_view& v) {
+  v.f = valid ? flag_load(P.flags + i) : 0u;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint64_t* r = P.recs + (valid ? i : 0) * R_WORDS;
+  const bool agg = valid && v.f >= F_AGG, inc = valid && v.f >= F_INCL;
+  v.meta = agg ? (uint32_t)st_load(r + R_META) : 0u;
+#pragma unroll
+  for (uint32_t q = 0; q < NENT / 2; q++) v.ent[q] = agg ? st_load(r + R_ENT0 + q) : 0;
+#pragma unroll
+  for (uint32_t o = 0; o < NOUT; o++)
+#pragma unroll
+    for (uint32_t w = 0; w < 2; w++) v.out[o][w] = agg ? st_load(r + R_OUT0 + 2 * o + w) : 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 5; q++) v.inc[q] = inc ? st_load(r + R_INC + q) : 0;
+}
+
+// Compose the uniform exact state s through segments w0 .. w0+n-1 (lane l
+// holds segment w0+l in v). Only segments the state enters are visited (the
+// others pass it through unchanged). Stops at the first entered segment whose
+// record is missing or whose aggregate does not contain the entry. Lane l's
+// `post` receives the exact state after segment w0+l for every l < return.
+XYWS_DEV uint32_t compose_window(const st_params& P, cstate& s, uint64_t w0, uint32_t n,
+                                 const seg_view& v, uint32_t lane, cstate& post) {
+  uint32_t done = n;
+  uint64_t path = 0;  // lanes whose segment the state entered
+  for (uint32_t guard = 0; guard < 64; guard++) {
+    if ((s.st & S_PARTIAL) || s.X >= P.hi) break;
+    const uint64_t t64 = s.X / SEG - w0;
+    if (t64 >= n) break;
+    const uint32_t t = (uint32_t)t64;
+    const uint32_t ft = rl32(v.f, t);
+    if (ft >= F_INCL) {
+      s.X = rl64(v.inc[0], t); s.cov_ps = rl64(v.inc[1], t); s.cov_start = rl64(v.inc[2], t);
+      const uint64_t kw = rl64(v.inc[3], t);
+      s.cov_kw = (uint32_t)kw; s.st = (uint32_t)(kw >> 32); s.cnt = rl64(v.inc[4], t);
+    } else if (ft >= F_AGG) {
+      const uint64_t tss = (w0 + t) * SEG;
+      const uint32_t xr = (uint32_t)(s.X - tss);
+      const uint32_t ne = rl32(v.meta, t) & 0xFF;
+      uint32_t e = 0xFFFFFFFFu;
+#pragma unroll
+      for (uint32_t q = 0; q < NENT; q++) {  // constant indices: no scratch
+        const uint32_t eq = rl32((uint32_t)(v.ent[q / 2] >> (32 * (q % 2))), t);
+        if (e == 0xFFFFFFFFu && q < ne && (eq & 0xFFFFu) == xr) e = eq;
+      }
+      if (e == 0xFFFFFFFFu) { done = t; break; }
+      const uint32_t oc = e >> 29;
+      uint64_t w0v = 0, w1v = 0;
+#pragma unroll
+      for (uint32_t o = 0; o < NOUT; o++)
+        if (o == oc) { w0v = v.out[o][0]; w1v = v.out[o][1]; }
+      w0v = rl64(w0v, t);
+      w1v = rl64(w1v, t);
+      s.X = w0v;
+      s.cov_ps = tss + (w1v & 0xFFFFF);
+      s.cov_start = s.cov_ps - ((w1v >> 20) & 0xF);
+      s.cov_kw = (uint32_t)(w1v >> 32);
+      s.cnt += (e >> 16) & 0x1FFF;
+      s.st = 0;
+    } else {
+      done = t;
+      break;
+    }
+    path |= 1ull << t;
+    if (lane == t) post = s;
+  }
+  // lanes off the path carry the state of the last path lane before them
+  // (or the incoming state, which every lane already holds in `post`)
+  const uint64_t below = path & ((lane == 63) ? ~0ull : ((2ull << lane) - 1));
+  const int src = below ? 63 - __builtin_clzll(below) : -1;
+  {
+    const int a = (src >= 0 ? src : (int)lane) * 4;
+    cstate q;
+    q.X = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(post.X >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)post.X);
+    q.cov_ps = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(post.cov_ps >> 32)) << 32) |
+               (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)post.cov_ps);
+    q.cov_start = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(post.cov_start >> 32)) << 32) |
+                  (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)post.cov_start);
+    q.cnt = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(post.cnt >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)post.cnt);
+    q.cov_kw = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)post.cov_kw);
+    q.st = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)post.st);
+    if (src >= 0) post = q;
+  }
+  return done;
+}
+
+// Lanes l < k publish their post-state as segment w0+l's inclusive record
+// (skipping segments already inclusive).
+XYWS_DEV void publish_window(const st_params& P, uint64_t w0, uint32_t k, uint32_t lane,
+                             const seg_view& v, const cstate& post) {
+  const bool mine = lane < k && v.f < F_INCL;
+  if (mine) {
+    uint64_t* r = P.recs + (w0 + lane) * R_WORDS;
+    st_store(r + R_INC + 0, post.X);
+    st_store(r + R_INC + 1, post.cov_ps);
+    st_store(r + R_INC + 2, post.cov_start);
+    st_store(r + R_INC + 3, (uint64_t)post.cov_kw | ((uint64_t)post.st << 32));
+    st_store(r + R_INC + 4, post.cnt);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (mine) __hip_atomic_store(P.flags + w0 + lane, F_INCL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+XYWS_DEV cstate wave_rec_incl(const st_params& P, int64_t j) {
+  if (j < 0) return initial_state(P);
+  return rec_incl(P.recs + (uint64_t)j * R_WORDS);
+}
+
+// Exact state before segment `seg`, computed by the whole wave (result uniform).
+XYWS_DEV cstate lookback_wave(const st_params& P, uint64_t seg, uint32_t lane) {
+  uint32_t* err = P.head + 1;
+  if (seg == 0) return initial_state(P);
+  // nearest inclusive predecessor (j = -1: the batch start)
+  int64_t j = -1;
+  if (stat_on(P)) stat_add(P, ST_LB, 1);
+  for (int64_t b = (int64_t)seg - 1; b >= 0; b -= 64) {
+    const int64_t i = b - (int64_t)lane;
+    const uint32_t f = i >= 0 ? flag_load(P.flags + i) : F_INCL;
+    const uint64_t m = __ballot(f >= F_INCL);
+    if (m) { j = b - (int64_t)__builtin_ctzll(m); break; }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  cstate s = wave_rec_incl(P, j);
+  uint64_t w0 = (uint64_t)(j + 1);
+  for (uint32_t guard = 0; w0 < seg && guard < 1u << 20; guard++) {
+    const uint32_t n = seg - w0 < 64 ? (uint32_t)(seg - w0) : 64u;
+    seg_view v;
+    load_view(P, w0 + lane, lane < n, v);
+    cstate post = s;
+    const uint32_t k = compose_window(P, s, w0, n, v, lane, post);
+    publish_window(P, w0, k, lane, v, post);
+    if (stat_on(P)) { stat_add(P, ST_LB_WIN, 1); stat_add(P, ST_LB_SEG, k); }
+    w0 += k;
+    if (k < n) {  // segment w0 needs its own inclusive record (or its aggregate)
+      if (stat_on(P)) stat_add(P, ST_LB_STALL, 1);
+      // exact header chase through segment w0 in global memory (headers are
+      // immutable); only a long chase waits for the owner's inclusive record
+      bool inc = false;
+      cstate c = s;
+      chase_global(P, c, (w0 + 1) * SEG, 16, &inc);
+      if (!inc) {
+        s = c;
+        if (lane == 0) pub_incl(P, w0, s);
+        w0 += 1;
+        continue;
+      }
+      if (stat_on(P)) stat_add(P, ST_LB_WAITINC, 1);
+      if (!flag_wait(P.flags + w0, F_INCL, err)) { s.X = ~0ull; break; }
+      s = rec_incl(P.recs + w0 * R_WORDS);
+      w0 += 1;
+    }
+  }
+  return s;
+}
+
+// After resolving segment `seg` with exact output o: publish the inclusive
+// records of the successors the wave can compose from their aggregates.
+XYWS_DEV void help_wave(const st_params& P, uint64_t seg, cstate o, uint32_t lane) {
+  uint64_t w0 = seg + 1;
+  for (uint32_t round = 0; round < HELP / 64 && w0 < P.nseg; round++) {
+    const uint32_t n = P.nseg - w0 < 64 ? (uint32_t)(P.nseg - w0) : 64u;
+    seg_view v;
+    load_view(P, w0 + lane, lane < n, v);
+    // stop at segments already inclusive (someone else is ahead) or not yet aggregated
+    const uint64_t stop = __ballot(lane < n && (v.f < F_AGG || v.f >= F_INCL));
+    const uint32_t lim = stop ? (uint32_t)__builtin_ctzll(stop) : n;
+    cstate post = o;
+    const uint32_t k = compose_window(P, o, w0, lim, v, lane, post);
+    publish_window(P, w0, k, lane, v, post);
+    if (stat_on(P)) { stat_add(P, ST_HELP_WIN, 1); stat_add(P, ST_HELP_SEG, k); }
+    if (k < n) break;
+    w0 += n;
+  }
+}
+
+XYWS_DEV void write_frame(const st_params& P, uint64_t ord, uint64_t start, const hdr_info& h,
+                          uint64_t ps, int32_t hdr_shift) {
+  if (!P.frames || ord >= P.cap) return;
+  xyws_frame f;
+  f.frame_off = (int64_t)(start - P.lo) - hdr_shift;
+  f.payload_off = (int64_t)(ps - P.lo);
+  f.payload_len = h.plen;
+  f.key[0] = (uint8_t)h.key; f.key[1] = (uint8_t)(h.key >> 8);
+  f.key[2] = (uint8_t)(h.key >> 16); f.key[3] = (uint8_t)(h.key >> 24);
+  f.flags = h.flags;
+  f.hdr_len = (uint8_t)h.hlen;
+  f.status = (uint8_t)(h.status | (sat_add(ps, h.plen) > P.hi ? XYWS_ST_PAYLOAD_INCOMPLETE : 0));
+  f.reserved = 0;
+  P.frames[ord] = f;
+}
+
+XYWS_DEV uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (uint32_t o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// XOR words for the 16-byte chunk at segment offset a. Entries are contiguous
+// frames sorted by start; g = the last entry starting at or before a. Common
+// case: one frame's payload covers the whole chunk.
+XYWS_DEV u32x4 chunk_xor(const st_lds& L, uint32_t nfl, uint32_t g, uint32_t a) {
+  const fent e = L.flist[g];
+  if (e.ps <= a && e.end >= a + 16) return u32x4{e.kw, e.kw, e.kw, e.kw};
+  u32x4 w = {0u, 0u, 0u, 0u};
+  for (uint32_t h = g; h < nfl; h++) {
+    const fent f = L.flist[h];
+    if (h != g && f.start >= a + 16) break;
+    w.x |= f.kw & range_mask(a, f.ps, f.end);
+    w.y |= f.kw & range_mask(a + 4, f.ps, f.end);
+    w.z |= f.kw & range_mask(a + 8, f.ps, f.end);
+    w.w |= f.kw & range_mask(a + 12, f.ps, f.end);
+  }
+  return w;
+}
+
+// ---------------------------------------------------------------- kernel
+__global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
+  __shared__ st_lds L;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint32_t* err = P.head + 1;
+  const bool want_unmasked = (P.opts & XYWS_OPT_UNMASKED_HINT) != 0;
+  const bool parse_only = (P.opts & XYWS_OPT_PARSE_ONLY) != 0;
+  const uint64_t lo = P.lo, hi = P.hi;
+
+  for (;;) {
+    if (tid == 0) L.seg_id = atomicAdd(P.head, 1u);
+    __syncthreads();
+    const uint64_t seg = L.seg_id;
+    if (seg >= P.nseg) break;
+    const uint64_t ss = seg * SEG, se = ss + SEG;
+
+    // ---- 1. loads: the whole segment into registers -----------------------
+    // Buffer descriptor over [ss, ss + round16(hi - ss)) capped at SEG + 16:
+    // the base and range live in SGPRs, each lane keeps one 32-bit offset, and
+    // chunks past the batch read as zero (hardware range check).
+    const uint64_t room = hi - ss;
+    const uint32_t nrec = room >= SEG + 16 ? SEG + 16 : (uint32_t)((room + 15) & ~15ull);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(P.base + ss, 0, nrec, 0x00020000);
+    const uint32_t voff = tid * 16u;
+    u32x4 d[CHS];
+#pragma unroll
+    for (uint32_t k = 0; k < CHS; k++) d[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * NT * 16u, 0);
+    u32x4 halo = {0u, 0u, 0u, 0u};
+    if (tid == 0) halo = __builtin_amdgcn_raw_buffer_load_b128(rs, 0, SEG, 0);
+    if (tid == 0) { L.nsurv = 0; L.overflow = 0; }
+
+    // ---- 1b. per sub-tile: LDS copy, prefilter, candidates -> survivors ----
+#pragma nounroll
+    for (uint32_t s = 0; s < NSUB; s++) {
+      const uint64_t ts = ss + (uint64_t)s * SUB, te = ts + SUB;
+      __syncthreads();  // previous sub-tile fully consumed
+#pragma unroll
+      for (uint32_t k = 0; k < CHSUB; k++) {
+        const u32x4 v = s == 0 ? d[k] : d[CHSUB + k];
+        *reinterpret_cast<u32x4*>(&L.sub[(k * NT + tid) * 16u]) = v;
+      }
+      if (tid == 0) {
+        const u32x4 v = s == 0 ? d[CHSUB] : halo;
+        *reinterpret_cast<u32x4*>(&L.sub[SUB]) = v;
+      }
+      __syncthreads();
+      // prefilter: lane owns sub-tile positions [tid*128, tid*128+128)
+      uint64_t cand[2] = {0, 0};
+      {
+        const uint32_t p0 = tid * 128u;
+        uint32_t w = *reinterpret_cast<const uint32_t*>(&L.sub[p0]);
+#pragma unroll
+        for (uint32_t i = 0; i < 32; i++) {
+          const uint32_t wn = *reinterpret_cast<const uint32_t*>(&L.sub[p0 + 4 * i + 4]);
+          const uint32_t b1s = (w >> 8) | (wn << 24);  // byte t = byte at position 4i+t+1
+          const uint32_t rsv_ok = ~((w & 0x70707070u) + 0x70707070u) & 0x80808080u;
+          const uint32_t bad_op = ((w << 5) | ((w & (w >> 1)) << 7)) & 0x80808080u;
+          const uint32_t m_ok = (want_unmasked ? ~b1s : b1s) & 0x80808080u;
+          const uint32_t c = rsv_ok & ~bad_op & m_ok;
+          const uint32_t nib = ((c >> 7) | (c >> 14) | (c >> 21) | (c >> 28)) & 0xFu;
+          cand[i >> 4] |= (uint64_t)nib << (4 * (i & 15));
+          w = wn;
+        }
+        const uint64_t a0 = ts + p0;
+#pragma unroll
+        for (uint32_t h = 0; h < 2; h++) {
+          const uint64_t st = a0 + 64 * h;
+          uint64_t m = ~0ull;
+          if (st + 64 > hi) m = (st >= hi) ? 0 : ((1ull << (hi - st)) - 1);
+          if (st < lo) m &= (lo - st >= 64) ? 0 : ~((1ull << (lo - st)) - 1);
+          cand[h] &= m;
+          L.bits[2 * tid + h] = cand[h];
+        }
+      }
+      __syncthreads();
+      // full parse of the lane's candidates
+      uint64_t surv[2] = {0, 0};
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        uint64_t m = cand[h];
+        while (m) {
+          const uint32_t b = __builtin_ctzll(m);
+          m &= m - 1;
+          const uint32_t prel = tid * 128u + 64u * h + b;
+          const uint64_t pabs = ts + prel;
+          hdr_info hh = header_lds(L.sub, prel, pabs, hi);
+          if (!plausible(hh, L.sub[prel + 1])) continue;
+          const uint64_t nx = sat_add(pabs + hh.hlen, hh.plen);
+          if (nx > hi) continue;
+          bool ok = true;
+          if (nx < te) {
+            const uint32_t nr = (uint32_t)(nx - ts);
+            ok = (L.bits[nr >> 6] >> (nr & 63)) & 1ull;
+          }
+          if (ok) surv[h] |= 1ull << b;
+        }
+      }
+      // ordered append: block-exclusive scan of per-lane survivor counts
+      const uint32_t c0 = __popcll(surv[0]), c1 = __popcll(surv[1]);
+      const uint32_t v = c0 + c1;
+      uint32_t x = v;
+#pragma unroll
+      for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (lane == 63) L.scan[wave] = x;
+      __syncthreads();
+      uint32_t wb = 0, tot = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < 4; i++) {
+        const uint32_t si = L.scan[i];
+        if (i < wave) wb += si;
+        tot += si;
+      }
+      const uint32_t base_n = L.nsurv;
+      const bool fits = base_n + tot <= SMAX;
+      if (fits) {
+        uint32_t r = base_n + wb + x - v;
+#pragma unroll
+        for (uint32_t h = 0; h < 2; h++) {
+          uint64_t m = surv[h];
+          while (m) {
+            const uint32_t b = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t prel = tid * 128u + 64u * h + b;
+            hdr_info hh = header_lds(L.sub, prel, ts + prel, hi);
+            L.s_pos[r] = s * SUB + prel;
+            L.s_nrel[r] = clamp_rel(sat_add(ts + prel + hh.hlen, hh.plen), ss);
+            L.s_key[r] = hh.key;
+            L.s_hlen[r] = (uint8_t)hh.hlen;
+            r++;
+          }
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        if (fits) L.nsurv = base_n + tot;
+        else L.overflow = 1;
+      }
+    }
+    __syncthreads();
+
+    // ---- 2. link survivors ------------------------------------------------
+    const uint32_t nsurv = L.overflow ? 0u : L.nsurv;
+    for (uint32_t i = tid; i < nsurv; i += NT) {
+      const uint32_t nr = L.s_nrel[i];
+      uint16_t nn = N_EXIT;
+      if (nr < SEG) {
+        uint32_t x = i + 1, y = nsurv;  // successor lies after i: search (i, nsurv)
+        while (x < y) {
+          const uint32_t m = (x + y) >> 1;
+          if (L.s_pos[m] < nr) x = m + 1; else y = m;
+        }
+        nn = (x < nsurv && L.s_pos[x] == nr) ? (uint16_t)x : N_DEAD;
+      }
+      L.s_nxt[i] = nn;
+      L.s_out[i] = O_NONE;
+      L.s_ord[i] = ORD_NONE;
+    }
+    __syncthreads();
+
+    // ---- 2b/3/4/5a: wave 0: graph walk + aggregate (lane 0), look-back
+    //      (wave), own resolution (lane 0), helping (wave) ------------------------
+    if (wave == 0) {
+      if (lane == 0) {
+        uint64_t* rec = P.recs + seg * R_WORDS;
+        uint32_t nout = 0, nent = 0;
+        uint64_t (&outs)[NOUT][4] = L.outs;
+        uint32_t (&ents)[NENT] = L.ents;
+        // memoized walk in position order
+        for (uint32_t i = 0; i < nsurv; i++) {
+          if (L.s_out[i] != O_NONE) continue;
+          uint32_t j = i, steps = 0;
+          uint8_t oc;
+          uint32_t remj = 0;
+          for (;;) {  // to the first node with a known outcome, the exit or a dead end
+            steps++;
+            const uint16_t n = L.s_nxt[j];
+            if (n == N_EXIT) {
+              if (nout < NOUT) {
+                const uint64_t p = ss + L.s_pos[j];
+                const uint64_t ps = p + L.s_hlen[j];
+                outs[nout][0] = L.s_nrel[j] == 0xFFFFFFFFu ? ~0ull : ss + L.s_nrel[j];
+                outs[nout][1] = ps;
+                outs[nout][2] = p;
+                outs[nout][3] = aligned_key(L.s_key[j], ps, 0);
+                oc = (uint8_t)nout++;
+              } else {
+                oc = O_UNREC;
+              }
+              remj = 0;
+              j = 0xFFFFFFFFu;
+              break;
+            }
+            if (n == N_DEAD) { oc = O_DEAD; j = 0xFFFFFFFFu; break; }
+            if (L.s_out[n] != O_NONE) { oc = L.s_out[n]; remj = L.s_rem[n]; j = n; break; }
+            j = n;
+          }
+          // second walk: outcome, remaining count, primary ordinals
+          const bool primary = (oc < NOUT) && (j == 0xFFFFFFFFu);
+          uint32_t k = i;
+          for (uint32_t q = 0; q < steps; q++) {
+            L.s_out[k] = oc;
+            L.s_rem[k] = (uint16_t)(steps - q + remj);
+            if (primary) L.s_ord[k] = (uint16_t)q;
+            if (oc < NOUT && nent < NENT)
+              ents[nent++] = L.s_pos[k] | ((steps - q + remj) << 16) | ((uint32_t)oc << 29);
+            k = L.s_nxt[k];
+          }
+        }
+        // publish the aggregate
+        st_store(rec + R_META, (uint64_t)nent | ((uint64_t)nout << 8) | ((uint64_t)L.overflow << 16));
+        for (uint32_t q = 0; q < nent; q += 2)
+          st_store(rec + R_ENT0 + q / 2, (uint64_t)ents[q] | (q + 1 < nent ? (uint64_t)ents[q + 1] << 32 : 0));
+        for (uint32_t o = 0; o < nout; o++) {
+          st_store(rec + R_OUT0 + 2 * o, outs[o][0]);
+          st_store(rec + R_OUT0 + 2 * o + 1, (outs[o][1] - ss) | ((outs[o][1] - outs[o][2]) << 20) |
+                                                 (outs[o][3] << 32));
+        }
+        flag_publish(P.flags + seg, F_AGG);
+      }
+
+      // ---- 4. look-back (whole wave): exact state before this segment
+      cstate s = lookback_wave(P, seg, lane);
+
+      // ---- 5a. own exact chain (lane 0): primary-walk suffix or exact chase
+      cstate o = s;
+      if (lane == 0) {
+        uint32_t mode = 0, ordx = 0, outx = 0, npre = 0;
+        if (!(s.st & S_PARTIAL) && s.X < se && s.X < hi) {
+          const uint32_t xr = (uint32_t)(s.X - ss);
+          uint32_t x = 0, y = nsurv;
+          while (x < y) {
+            const uint32_t m = (x + y) >> 1;
+            if (L.s_pos[m] < xr) x = m + 1; else y = m;
+          }
+          bool hit = x < nsurv && L.s_pos[x] == xr && L.s_out[x] < NOUT;
+          if (hit) {  // non-primary entry: walk its prefix up to the primary walk it joins
+            uint32_t k = x;
+            while (L.s_ord[k] == ORD_NONE && npre < 64) { L.s_ord_pre[npre++] = (uint16_t)k; k = L.s_nxt[k]; }
+            if (L.s_ord[k] == ORD_NONE) hit = false;
+            else x = k;
+          }
+          if (hit) {
+            mode = 1;
+            ordx = L.s_ord[x];
+            outx = L.s_out[x];
+            o.X = L.outs[outx][0]; o.cov_ps = L.outs[outx][1]; o.cov_start = L.outs[outx][2];
+            o.cov_kw = (uint32_t)L.outs[outx][3];
+            o.cnt = s.cnt + L.s_rem[x] + npre;
+            o.st = 0;
+          } else {
+            mode = 2;
+            npre = 0;
+            bool inc = false;
+            chase_global(P, o, se, 0xFFFFFFFFu, &inc);
+          }
+        }
+        L.in = s;
+        L.out = o;
+        L.mode = mode;
+        L.ord_x = ordx;
+        L.out_x = outx;
+        L.npre = npre;
+        pub_incl(P, seg, o);
+        if (stat_on(P)) {
+          stat_add(P, mode == 2 ? ST_MODE2 : ST_MODE1, 1);
+          stat_add(P, ST_NSURV, nsurv);
+        }
+      }
+      o = bcast_state(o);  // lane 0's result to the wave
+
+      // ---- helping (whole wave): carry the exact state through successors
+      help_wave(P, seg, o, lane);
+    }
+    __syncthreads();
+
+    // ---- 5b/6. frame-list passes, XOR into registers -------------------------
+    const cstate sin = L.in;
+    const uint32_t mode = L.mode;
+    uint32_t changed = 0;
+
+    // the carried-header frame of the batch is described by segment 0
+    if (seg == 0 && tid == 0 && (sin.st & S_HDRCARRY) && !(sin.st & S_PARTIAL)) {
+      hdr_info hh = header_carried(P.base, lo, hi, P.cin);
+      write_frame(P, 0, lo, hh, sin.cov_ps, (int32_t)P.cin->hdr_len);
+    }
+    if (tid == 0) {
+      L.nfl = 0;
+      if (!(sin.st & (S_NOCOV | S_PARTCARRY))) {  // covering entry: frame begun before ss
+        fent e;
+        e.start = 0;
+        e.ps = clamp_rel(sin.cov_ps, ss);
+        e.end = clamp_rel(sin.X, ss);
+        e.kw = sin.cov_kw;
+        L.flist[0] = e;
+        L.nfl = 1;
+      }
+      L.fbase = sin.cnt;
+      L.chase_X = sin.X;
+      L.pass_done = (mode != 2);
+    }
+    __syncthreads();
+    if (mode == 1) {
+      const uint32_t ox = L.ord_x, oc = L.out_x, npre = L.npre;
+      if (tid < npre) {
+        const uint32_t i = L.s_ord_pre[tid];
+        const uint64_t p = ss + L.s_pos[i];
+        const uint64_t ps = p + L.s_hlen[i];
+        fent e;
+        e.start = L.s_pos[i];
+        e.ps = (uint32_t)(ps - ss);
+        e.end = L.s_nrel[i];
+        e.kw = aligned_key(L.s_key[i], ps, 0);
+        L.flist[L.nfl + tid] = e;
+        if (P.frames) {
+          hdr_info hh = header_global(P.base, p, hi);
+          write_frame(P, sin.cnt + tid, p, hh, ps, 0);
+        }
+      }
+      const uint32_t base_n = L.nfl + npre;
+      const uint64_t cbase = sin.cnt + npre;
+      uint32_t cnt = 0;
+      for (uint32_t i = tid; i < nsurv; i += NT) {
+        const uint16_t od = L.s_ord[i];
+        if (L.s_out[i] == oc && od != ORD_NONE && od >= ox) {
+          const uint64_t p = ss + L.s_pos[i];
+          const uint64_t ps = p + L.s_hlen[i];
+          fent e;
+          e.start = L.s_pos[i];
+          e.ps = (uint32_t)(ps - ss);
+          e.end = L.s_nrel[i];
+          e.kw = aligned_key(L.s_key[i], ps, 0);
+          L.flist[base_n + (od - ox)] = e;
+          if (P.frames) {
+            hdr_info hh = header_global(P.base, p, hi);
+            write_frame(P, cbase + (od - ox), p, hh, ps, 0);
+          }
+          cnt++;
+        }
+      }
+      cnt = wave_sum(cnt);
+      if (lane == 0) L.scan[wave] = cnt;
+      __syncthreads();
+      if (tid == 0) L.nfl = base_n + L.scan[0] + L.scan[1] + L.scan[2] + L.scan[3];
+    }
+
+    for (;;) {
+      if (mode == 2 && tid == 0) {  // exact chase in global memory, FCAP entries per pass
+        uint64_t X = L.chase_X, ord = L.fbase;
+        uint32_t n = L.nfl;
+        const uint64_t stop = se < hi ? se : hi;
+        while (X < stop && n < FCAP) {
+          hdr_info hh = header_global(P.base, X, hi);
+          if (!hh.hlen) { X = ~0ull; break; }
+          const uint64_t ps = X + hh.hlen;
+          fent e;
+          e.start = (uint32_t)(X - ss);
+          e.ps = (uint32_t)(ps - ss);
+          e.end = clamp_rel(sat_add(ps, hh.plen), ss);
+          e.kw = aligned_key(hh.key, ps, 0);
+          L.flist[n++] = e;
+          write_frame(P, ord++, X, hh, ps, 0);
+          X = sat_add(ps, hh.plen);
+        }
+        L.nfl = n;
+        L.fbase = ord;
+        L.chase_X = X;
+        L.pass_done = !(X < stop);
+      }
+      __syncthreads();
+      const uint32_t nfl = L.nfl;
+      if (!parse_only && nfl) {
+        uint32_t g = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < CHS; k++) {
+          const uint32_t a = (k * NT + tid) * 16u;  // increases with k: g only moves forward
+          while (g + 1 < nfl && L.flist[g + 1].start <= a) g++;
+          const u32x4 x = chunk_xor(L, nfl, g, a);
+          if ((x.x | x.y | x.z | x.w) != 0u) {
+            d[k] ^= x;
+            changed |= 1u << k;
+          }
+        }
+      }
+      const uint32_t done = L.pass_done;
+      __syncthreads();
+      if (done) break;
+      if (tid == 0) {  // next pass: the last frame becomes the covering entry
+        fent e = L.flist[L.nfl - 1];
+        e.start = 0;
+        L.flist[0] = e;
+        L.nfl = 1;
+      }
+      __syncthreads();
+    }
+
+    // ---- 6b. store changed chunks ------------------------------------------
+    if (!parse_only) {
+#pragma unroll
+      for (uint32_t k = 0; k < CHS; k++) {
+        if (!((changed >> k) & 1u)) continue;
+        const uint64_t a = ss + (k * NT + tid) * 16u;
+        if (a >= lo && a + 16 <= hi) {
+          __builtin_amdgcn_raw_buffer_store_b128(d[k], rs, voff, k * NT * 16u, 0);
+        } else {  // edge chunk: only the caller's bytes, only changed ones
+          const uint32_t w[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
+          for (uint32_t t = 0; t < 16; t++) {
+            const uint64_t q = a + t;
+            const uint8_t nb = (uint8_t)(w[t >> 2] >> (8u * (t & 3u)));
+            if (q >= lo && q < hi && P.base[q] != nb) P.base[q] = nb;
+          }
+        }
+      }
+    }
+
+    // ---- last segment: frame count + carry out --------------------------------
+    if (seg == P.nseg - 1 && tid == 0) {
+      const cstate o = L.out;
+      if (P.nframes) *P.nframes = o.cnt;
+      if (P.cout) {
+        xyws_carry c;
+        for (int i = 0; i < 64; i++) reinterpret_cast<uint8_t*>(&c)[i] = 0;
+        c.frames_total = P.cin->frames_total + o.cnt;
+        if (o.st & S_PARTIAL) {
+          uint32_t n = 0;
+          if (o.st & S_PARTCARRY) {
+            for (; n < P.cin->hdr_len; n++) c.hdr[n] = P.cin->hdr[n];
+            for (uint64_t q = lo; q < hi && n < 14; q++) c.hdr[n++] = P.base[q];
+          } else {
+            for (uint64_t q = o.X; q < hi && n < 14; q++) c.hdr[n++] = P.base[q];
+          }
+          c.hdr_len = (uint8_t)n;
+        } else if (o.X > hi && !(o.st & S_NOCOV)) {
+          if (o.st & S_CARRIED) {
+            c.payload_remaining = P.cin->payload_remaining - (hi - lo);
+            c.phase = P.cin->phase + (hi - lo);
+            for (int i = 0; i < 4; i++) c.key[i] = P.cin->key[i];
+          } else {
+            hdr_info hh;
+            if (o.st & S_HDRCARRY) {
+              hh = header_carried(P.base, lo, hi, P.cin);
+            } else {
+              hh = header_global(P.base, o.cov_start, hi);
+            }
+            c.payload_remaining = hh.plen - (hi - o.cov_ps);
+            c.phase = hi - o.cov_ps;
+            c.key[0] = (uint8_t)hh.key; c.key[1] = (uint8_t)(hh.key >> 8);
+            c.key[2] = (uint8_t)(hh.key >> 16); c.key[3] = (uint8_t)(hh.key >> 24);
+          }
+        }
+        *P.cout = c;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Empty batch: the state passes through unchanged.
+__global__ void k_stream_empty(const xyws_carry* cin, xyws_carry* cout, uint64_t* nframes) {
+  if (threadIdx.x) return;
+  if (nframes) *nframes = 0;
+  if (cout) {
+    xyws_carry c;
+    if (cin) c = *cin;
+    else for (int i = 0; i < 64; i++) reinterpret_cast<uint8_t*>(&c)[i] = 0;
+    *cout = c;
+  }
+}
+
+constexpr uint64_t HEAD_BYTES = 256;  // [0] ticket, [1] error, [64..128) carry snapshot, [128..256) stats
+
+int occupancy_grid() {
+  static int cached = 0;
+  if (cached) return cached;
+  int dev = 0, cus = 256, per = 2;
+  (void)hipGetDevice(&dev);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_stream_fused, NT, 0) != hipSuccess || per < 1)
+    per = 2;
+  cached = cus * per;
+  return cached;
+}
+
+}  // namespace
+
+void stream_scratch_init(stream_scratch* s) {
+  s->mem = nullptr;
+  s->bytes = 0;
+  s->max_tiles = 0;
+}
+
+void stream_scratch_free(stream_scratch* s) {
+  if (s->mem) (void)hipFree(s->mem);
+  s->mem = nullptr;
+  s->bytes = 0;
+  s->max_tiles = 0;
+}
+
+static uint64_t flags_bytes(uint64_t n) { return (n * 4 + 255) & ~255ull; }
+
+static int scratch_grow(stream_scratch* s, uint64_t segs) {
+  if (s->mem && segs <= s->max_tiles) return XYWS_OK;
+  const uint64_t want = segs < 64 ? 64 : segs;
+  const uint64_t bytes = HEAD_BYTES + flags_bytes(want) + want * R_WORDS * 8;
+  void* m = nullptr;
+  if (hipMalloc(&m, bytes) != hipSuccess) return XYWS_ERR_NOMEM;
+  if (s->mem) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(s->mem);
+  }
+  s->mem = m;
+  s->bytes = bytes;
+  s->max_tiles = want;
+  return hipMemset(m, 0, HEAD_BYTES) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
+}
+
+int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
+  return scratch_grow(s, (max_batch_bytes + 15 + SEG - 1) / SEG + 1);
+}
+
+int stream_scratch_stats(stream_scratch* s, uint64_t out[16]) {
+  if (!s->mem) return XYWS_ERR_INVALID;
+  if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
+  return hipMemcpy(out, static_cast<uint8_t*>(s->mem) + 128, 128, hipMemcpyDeviceToHost) == hipSuccess
+             ? XYWS_OK : XYWS_ERR_HIP;
+}
+
+uint32_t stream_scratch_error(stream_scratch* s) {
+  if (!s->mem) return 0;
+  uint32_t v[2] = {0, 0};
+  if (hipMemcpy(v, s->mem, 8, hipMemcpyDeviceToHost) != hipSuccess) return 0xFFFFFFFFu;
+  return v[1];
+}
+
+int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
+                        const xyws_carry* cin, xyws_carry* cout, xyws_frame* frames, uint64_t cap,
+                        uint64_t* nframes, uint32_t opts, hipStream_t stream) {
+  if (hi == lo) {
+    hipLaunchKernelGGL(k_stream_empty, dim3(1), dim3(64), 0, stream, cin, cout, nframes);
+    return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
+  }
+  const uint64_t nseg = (hi + SEG - 1) / SEG;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(stream, &cs);
+  if (nseg > s->max_tiles || !s->mem) {
+    if (cs != hipStreamCaptureStatusNone) return XYWS_ERR_CAPACITY;
+    const int rc = scratch_grow(s, nseg);
+    if (rc) return rc;
+  }
+  uint8_t* m = static_cast<uint8_t*>(s->mem);
+  st_params P;
+  P.base = base; P.lo = lo; P.hi = hi; P.nseg = nseg;
+  P.cout = cout; P.frames = frames; P.cap = cap; P.nframes = nframes;
+  P.head = reinterpret_cast<uint32_t*>(m);
+  P.flags = reinterpret_cast<uint32_t*>(m + HEAD_BYTES);
+  P.recs = reinterpret_cast<uint64_t*>(m + HEAD_BYTES + flags_bytes(s->max_tiles));
+  P.opts = opts;
+  // Ticket + flags zeroed every call (the error word [1] is sticky until read
+  // back). The carry is snapshotted first: dev_carry_in may alias
+  // dev_carry_out, which the last segment writes while others may still read
+  // the incoming carry.
+  xyws_carry* snap = reinterpret_cast<xyws_carry*>(m + 64);
+  if (hipMemsetAsync(P.head, 0, 4, stream) != hipSuccess) return XYWS_ERR_HIP;
+  if ((opts & XYWS_OPT_STATS) && hipMemsetAsync(m + 128, 0, 128, stream) != hipSuccess) return XYWS_ERR_HIP;
+  if (cin) {
+    if (hipMemcpyAsync(snap, cin, sizeof(xyws_carry), hipMemcpyDeviceToDevice, stream) != hipSuccess)
+      return XYWS_ERR_HIP;
+  } else if (hipMemsetAsync(snap, 0, sizeof(xyws_carry), stream) != hipSuccess) {
+    return XYWS_ERR_HIP;
+  }
+  P.cin = snap;
+  if (hipMemsetAsync(P.flags, 0, (nseg * 4 + 15) & ~15ull, stream) != hipSuccess) return XYWS_ERR_HIP;
+  int grid = occupancy_grid();
+  if ((uint64_t)grid > nseg) grid = (int)nseg;
+  hipLaunchKernelGGL(k_stream_fused, dim3(grid), dim3(NT), 0, stream, P);
+  return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
