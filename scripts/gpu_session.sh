@@ -28,7 +28,9 @@ for step in "$@"; do
     bench_c1) run bench_c1 300 python bench.py --config c1 --no-cpu ;;
     bench_c4) run bench_c4 300 python bench.py --config c4 --no-cpu ;;
     host) run bench_host 600 python bench.py --no-cpu --host-path --steps 5 ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$PWD/gpurun_out/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu ;;
+    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$PWD/gpurun_out/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
+    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$PWD/gpurun_out/pmc_write" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
