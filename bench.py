@@ -238,8 +238,8 @@ def main():
     avg_ms = sum(kernel_ms) / len(kernel_ms)
 
     if args.stats and rank == 0:  # one extra counted decode pair (keeps the step parity)
-        names = ["lookbacks", "lb_windows", "lb_segments", "lb_stalls", "lb_wait_incl",
-                 "help_windows", "help_segments", "mode1", "mode2", "survivors", "spins"]
+        names = ["exact_in", "spec", "no_spec", "valid", "slow", "recomputed", "no_anchor",
+                 "mode1", "mode2", "survivors", "spins"]
         for _ in range(2):
             dec.opts |= 0x100
             dec.decode(buf, cap=0, count=False, carry=False)

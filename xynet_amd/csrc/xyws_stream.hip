@@ -74,10 +74,10 @@ constexpr uint32_t SMAX = 1024;          // survivors tracked per segment
 constexpr uint32_t FCAP = SUB / 16;      // frame-list entries per pass (overlays the sub-tile)
 constexpr uint32_t NENT = 16;            // aggregate entry nodes (2 per record word)
 constexpr uint32_t NOUT = 8;             // aggregate outcomes (2 record words each)
-constexpr uint32_t HELP = 128;           // segments helped forward per resolution
 constexpr uint32_t SPIN = 1u << 24;      // bounded spins (~1 s)
 
-constexpr uint32_t F_AGG = 1, F_INCL = 2;
+constexpr uint32_t WIN = 64;             // segments seen by one look-back (one per lane)
+constexpr uint32_t BKT = 8;              // exits kept per target segment during speculation
 constexpr uint16_t N_EXIT = 0xFFFF, N_DEAD = 0xFFFE;
 constexpr uint8_t O_NONE = 0xFF, O_DEAD = 0xFE, O_UNREC = 0xFD;  // node outcome marks
 constexpr uint16_t ORD_NONE = 0xFFFF;
@@ -95,7 +95,13 @@ enum {
   R_META = 0,              // n_entries | n_outcomes << 8 | overflow << 16
   R_ENT0 = 1,              // NENT entries, two per word: pos (16) | rem (13) << 16 | outcome (3) << 29
   R_OUT0 = 9,              // NOUT outcomes x 2 words: exit; cov_ps - ss (20) | hlen (4) << 20 | kw << 32
-  R_INC = 32,              // X, cov_ps, cov_start, kw | st << 32, cnt
+  R_CI = 25,               // assumed input state  (X, cov_ps, cov_start, kw | st << 32)
+  R_CO = 29,               // output state computed from it
+  R_CN = 33,               // frames whose header starts in the segment (given the input)
+  R_EX = 34,               // exact output from the slow path (4 words)
+  R_EN = 38,               // exact frame count from the slow path
+  R_NA = 39,               // frame count aggregate (exact)
+  R_NI = 40,               // inclusive frame-count prefix
   R_WORDS = 64
 };
 
@@ -136,6 +142,9 @@ struct __attribute__((aligned(16))) st_lds {
   uint16_t s_ord_pre[64];     // non-primary prefix of the entry's path
   uint64_t outs[NOUT][4];     // aggregate outcomes: exit, cov_ps, cov_start, kw
   uint32_t ents[NENT];        // aggregate entries (packed as in the record)
+  uint32_t bk_n[WIN];         // speculation: exits landing in each window segment
+  uint32_t bk[WIN][BKT];
+  uint64_t nbase;             // frame ordinal of this segment's first frame
 };
 
 struct st_params {
@@ -146,8 +155,12 @@ struct st_params {
   xyws_frame* frames;
   uint64_t cap;
   uint64_t* nframes;
-  uint32_t* head;   // [0] ticket, [1] error word
-  uint32_t* flags;  // one per segment
+  uint32_t* head;   // [0] ticket, [1] error word, [2] finished segments, [4..5] u64 frame total
+  uint32_t* fA;     // per segment: aggregate published
+  uint32_t* fC;     // per segment: (assumed input, output) published
+  uint32_t* fV;     // per segment: 1 = output exact (validated), 2 = exact via the slow path
+  uint32_t* fN;     // per segment: 1 = count aggregate, 2 = inclusive count prefix
+  uint32_t* fP;     // per segment: 1 = assumed input == predecessor's published output, 2 = not
   uint64_t* recs;   // R_WORDS per segment
   uint32_t opts;
 };
@@ -155,7 +168,7 @@ struct st_params {
 // ---------------------------------------------------------------- debug counters
 // With XYWS_OPT_STATS the kernel counts resolution events into head[16..32)
 // (read back by xyws_debug_stats). Off by default: one uniform branch each.
-enum { ST_LB = 0, ST_LB_WIN, ST_LB_SEG, ST_LB_STALL, ST_LB_WAITINC, ST_HELP_WIN, ST_HELP_SEG,
+enum { ST_EXACT_IN = 0, ST_SPEC, ST_NOSPEC, ST_VALID, ST_SLOW, ST_RECOMP, ST_NOANCHOR,
        ST_MODE1, ST_MODE2, ST_NSURV, ST_SPINS, ST_NSTAT = 16 };
 
 // ---------------------------------------------------------------- hand-off
@@ -329,24 +342,32 @@ XYWS_DEV cstate initial_state(const st_params& P) {
   return s;
 }
 
-XYWS_DEV cstate rec_incl(const uint64_t* r) {
+XYWS_DEV cstate load_state(const uint64_t* r) {
   cstate s;
-  uint64_t w[5];
+  uint64_t w[4];
 #pragma unroll
-  for (int i = 0; i < 5; i++) w[i] = st_load(r + R_INC + i);
+  for (int i = 0; i < 4; i++) w[i] = st_load(r + i);
   s.X = w[0]; s.cov_ps = w[1]; s.cov_start = w[2];
-  s.cov_kw = (uint32_t)w[3]; s.st = (uint32_t)(w[3] >> 32); s.cnt = w[4];
+  s.cov_kw = (uint32_t)w[3]; s.st = (uint32_t)(w[3] >> 32); s.cnt = 0;
   return s;
 }
 
-XYWS_DEV void pub_incl(const st_params& P, uint64_t seg, const cstate& s) {
-  uint64_t* r = P.recs + seg * R_WORDS;
-  st_store(r + R_INC + 0, s.X);
-  st_store(r + R_INC + 1, s.cov_ps);
-  st_store(r + R_INC + 2, s.cov_start);
-  st_store(r + R_INC + 3, (uint64_t)s.cov_kw | ((uint64_t)s.st << 32));
-  st_store(r + R_INC + 4, s.cnt);
-  flag_publish(P.flags + seg, F_INCL);
+XYWS_DEV void store_state(uint64_t* r, const cstate& s) {
+  st_store(r + 0, s.X);
+  st_store(r + 1, s.cov_ps);
+  st_store(r + 2, s.cov_start);
+  st_store(r + 3, (uint64_t)s.cov_kw | ((uint64_t)s.st << 32));
+}
+
+XYWS_DEV bool same_state(const cstate& a, const cstate& b) {
+  return a.X == b.X && a.cov_ps == b.cov_ps && a.cov_start == b.cov_start &&
+         a.cov_kw == b.cov_kw && a.st == b.st;
+}
+
+// Exact output state of segment j (fV[j] = fv >= 1); j < 0: the batch start.
+XYWS_DEV cstate exact_out(const st_params& P, int64_t j, uint32_t fv) {
+  if (j < 0) return initial_state(P);
+  return load_state(P.recs + (uint64_t)j * R_WORDS + (fv == 2 ? R_EX : R_CO));
 }
 
 // Exact chase by header reads in global memory from s.X while s.X < lim.
@@ -367,10 +388,16 @@ XYWS_DEV void chase_global(const st_params& P, cstate& s, uint64_t lim, uint32_t
   if (!(s.st & S_PARTIAL) && s.X < stop) *incomplete = true;
 }
 
-// ---------------------------------------------------------------- wave-level look-back
+// ---------------------------------------------------------------- resolution
 XYWS_DEV uint32_t rl32(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
 XYWS_DEV uint64_t rl64(uint64_t v, uint32_t l) {
   return ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32) | rl32((uint32_t)v, l);
+}
+XYWS_DEV uint32_t bp32(uint32_t v, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4), (int)v);
+}
+XYWS_DEV uint64_t bp64(uint64_t v, uint32_t src) {
+  return ((uint64_t)bp32((uint32_t)(v >> 32), src) << 32) | bp32((uint32_t)v, src);
 }
 XYWS_DEV cstate bcast_state(const cstate& s) {  // lane 0's state to every lane
   cstate r;
@@ -378,191 +405,222 @@ XYWS_DEV cstate bcast_state(const cstate& s) {  // lane 0's state to every lane
   r.cnt = rl64(s.cnt, 0); r.cov_kw = rl32(s.cov_kw, 0); r.st = rl32(s.st, 0);
   return r;
 }
+XYWS_DEV void wave_sync() {  // order this wave's LDS accesses across lanes
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
-// One lane's view of segment i's status and records (sc1 loads).
-struct seg_view {
-  uint32_t f;              // flag
-  uint32_t meta;
-  uint64_t ent[NENT / 2];  // packed entry pairs
-  uint64_t out[NOUT][2];   // packed outcomes
-  uint64_t inc[5];
-};
+constexpr uint32_t S_NONE = 0x80000000u;  // "no speculation available" marker in cstate.st
 
-XYWS_DEV void load_view(const st_params& P, uint64_t i, bool valid, seg_view& v) {
-  v.f = valid ? flag_load(P.flags + i) : 0u;
+// Step A: the input state of segment k as the whole wave sees it.
+//  exact: the nearest validated predecessor's output already reaches k
+//         (every segment between it and k is covered by its last frame);
+//  else : speculation from the aggregates of the 63 preceding segments: an
+//         entry node is trusted when some outcome of an earlier segment (or
+//         the exact anchor) exits exactly onto it ("link support"); k takes
+//         the trusted outcome of the nearest segment that reaches it.
+XYWS_DEV cstate resolve_input(const st_params& P, st_lds& L, uint64_t k, uint32_t lane, bool& exact) {
+  exact = false;
+  if (k == 0) { exact = true; return initial_state(P); }
+  const uint64_t ts = k * SEG;
+  // A1: nearest predecessor with an exact output (j = -1: the batch start)
+  const int64_t j = (int64_t)k - 1 - (int64_t)lane;
+  const uint32_t fv = j >= 0 ? flag_load(P.fV + j) : (j == -1 ? 3u : 0u);
+  const uint64_t mv = __ballot(fv >= 1);
+  cstate E;
+  int64_t a = -2;
+  if (mv) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(mv);
+    a = (int64_t)k - 1 - (int64_t)l;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    E = exact_out(P, a, rl32(fv, l));
+    if ((E.st & S_PARTIAL) || E.X >= ts) { exact = true; E.cnt = 0; return E; }
+  }
+  // A2: speculation over the window [k-63, k] (lane l = segment k-63+l)
+  const int64_t w0 = (int64_t)k - (int64_t)(WIN - 1);
+  const int64_t g = w0 + (int64_t)lane;
+  // every window segment was ticketed before k and publishes its aggregate
+  // from local work only: wait for all of them (bounded)
+  bool have = g < 0 || flag_load(P.fA + g) >= 1;
+  for (uint32_t it = 0; !__all(have) && it < SPIN; it++) {
+    __builtin_amdgcn_s_sleep(1);
+    if (!have) have = flag_load(P.fA + g) >= 1;
+  }
+  have = have && g >= 0;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint64_t* r = P.recs + (valid ? i : 0) * R_WORDS;
-  const bool agg = valid && v.f >= F_AGG, inc = valid && v.f >= F_INCL;
-  v.meta = agg ? (uint32_t)st_load(r + R_META) : 0u;
+  const uint64_t* r = P.recs + (have ? (uint64_t)g : 0) * R_WORDS;
+  const uint32_t meta = have ? (uint32_t)st_load(r + R_META) : 0u;
+  uint64_t ent[NENT / 2], out[NOUT][2];
 #pragma unroll
-  for (uint32_t q = 0; q < NENT / 2; q++) v.ent[q] = agg ? st_load(r + R_ENT0 + q) : 0;
+  for (uint32_t q = 0; q < NENT / 2; q++) ent[q] = have ? st_load(r + R_ENT0 + q) : 0;
+#pragma unroll
+  for (uint32_t o = 0; o < NOUT; o++) {
+    out[o][0] = have ? st_load(r + R_OUT0 + 2 * o) : 0;
+    out[o][1] = have ? st_load(r + R_OUT0 + 2 * o + 1) : 0;
+  }
+  const uint32_t ne = meta & 0xFF, no = (meta >> 8) & 0xFF;
+  L.bk_n[lane] = 0;
+  wave_sync();
+  // every outcome exit that lands inside a later window segment is a link candidate
+#pragma unroll
+  for (uint32_t o = 0; o < NOUT; o++) {
+    if (o < no) {
+      const uint64_t x = out[o][0];
+      if (x < P.hi) {
+        const int64_t u = (int64_t)(x / SEG) - w0;
+        if (u > (int64_t)lane && u < (int64_t)WIN) {
+          const uint32_t slot = atomicAdd(&L.bk_n[u], 1u);
+          if (slot < BKT) L.bk[u][slot] = (uint32_t)(x - (uint64_t)(w0 + u) * SEG);
+        }
+      }
+    }
+  }
+  if (lane == 0 && a >= -1 && !(E.st & S_PARTIAL)) {  // the exact anchor's exit supports too
+    const int64_t u = (int64_t)(E.X / SEG) - w0;
+    if (E.X < P.hi && u >= 0 && u < (int64_t)WIN) {
+      const uint32_t slot = atomicAdd(&L.bk_n[u], 1u);
+      if (slot < BKT) L.bk[u][slot] = (uint32_t)(E.X - (uint64_t)(w0 + u) * SEG);
+    }
+  }
+  wave_sync();
+  // each segment: the first entry that some exit lands on -> its outcome
+  const uint32_t nb = L.bk_n[lane] < BKT ? L.bk_n[lane] : BKT;
+  uint32_t oc = 0xFFu;
+#pragma unroll
+  for (uint32_t q = 0; q < NENT; q++) {
+    const uint32_t e = (uint32_t)(ent[q / 2] >> (32 * (q % 2)));
+    if (oc == 0xFFu && q < ne) {
+      for (uint32_t b = 0; b < nb; b++)
+        if (L.bk[lane][b] == (e & 0xFFFFu)) { oc = e >> 29; break; }
+    }
+  }
+  uint64_t dX = 0, dW = 0;
 #pragma unroll
   for (uint32_t o = 0; o < NOUT; o++)
-#pragma unroll
-    for (uint32_t w = 0; w < 2; w++) v.out[o][w] = agg ? st_load(r + R_OUT0 + 2 * o + w) : 0;
-#pragma unroll
-  for (uint32_t q = 0; q < 5; q++) v.inc[q] = inc ? st_load(r + R_INC + q) : 0;
+    if (o == oc) { dX = out[o][0]; dW = out[o][1]; }
+  // k's input: the trusted outcome of the nearest earlier segment that reaches k
+  const uint64_t m = __ballot(oc != 0xFFu && lane < WIN - 1 && dX >= ts);
+  cstate I;
+  I.cnt = 0;
+  if (!m) { I.X = 0; I.cov_ps = 0; I.cov_start = 0; I.cov_kw = 0; I.st = S_NONE; return I; }
+  const uint32_t p = 63 - __builtin_clzll(m);
+  const uint64_t pss = (uint64_t)(w0 + (int64_t)p) * SEG;
+  const uint64_t w1 = rl64(dW, p);
+  I.X = rl64(dX, p);
+  I.cov_ps = pss + (w1 & 0xFFFFF);
+  I.cov_start = I.cov_ps - ((w1 >> 20) & 0xF);
+  I.cov_kw = (uint32_t)(w1 >> 32);
+  I.st = 0;
+  return I;
 }
 
-// Compose the uniform exact state s through segments w0 .. w0+n-1 (lane l
-// holds segment w0+l in v). Only segments the state enters are visited (the
-// others pass it through unchanged). Stops at the first entered segment whose
-// record is missing or whose aggregate does not contain the entry. Lane l's
-// `post` receives the exact state after segment w0+l for every l < return.
-XYWS_DEV uint32_t compose_window(const st_params& P, cstate& s, uint64_t w0, uint32_t n,
-                                 const seg_view& v, uint32_t lane, cstate& post) {
-  uint32_t done = n;
-  uint64_t path = 0;  // lanes whose segment the state entered
-  for (uint32_t guard = 0; guard < 64; guard++) {
-    if ((s.st & S_PARTIAL) || s.X >= P.hi) break;
-    const uint64_t t64 = s.X / SEG - w0;
-    if (t64 >= n) break;
-    const uint32_t t = (uint32_t)t64;
-    const uint32_t ft = rl32(v.f, t);
-    if (ft >= F_INCL) {
-      s.X = rl64(v.inc[0], t); s.cov_ps = rl64(v.inc[1], t); s.cov_start = rl64(v.inc[2], t);
-      const uint64_t kw = rl64(v.inc[3], t);
-      s.cov_kw = (uint32_t)kw; s.st = (uint32_t)(kw >> 32); s.cnt = rl64(v.inc[4], t);
-    } else if (ft >= F_AGG) {
-      const uint64_t tss = (w0 + t) * SEG;
-      const uint32_t xr = (uint32_t)(s.X - tss);
-      const uint32_t ne = rl32(v.meta, t) & 0xFF;
-      uint32_t e = 0xFFFFFFFFu;
-#pragma unroll
-      for (uint32_t q = 0; q < NENT; q++) {  // constant indices: no scratch
-        const uint32_t eq = rl32((uint32_t)(v.ent[q / 2] >> (32 * (q % 2))), t);
-        if (e == 0xFFFFFFFFu && q < ne && (eq & 0xFFFFu) == xr) e = eq;
-      }
-      if (e == 0xFFFFFFFFu) { done = t; break; }
-      const uint32_t oc = e >> 29;
-      uint64_t w0v = 0, w1v = 0;
-#pragma unroll
-      for (uint32_t o = 0; o < NOUT; o++)
-        if (o == oc) { w0v = v.out[o][0]; w1v = v.out[o][1]; }
-      w0v = rl64(w0v, t);
-      w1v = rl64(w1v, t);
-      s.X = w0v;
-      s.cov_ps = tss + (w1v & 0xFFFFF);
-      s.cov_start = s.cov_ps - ((w1v >> 20) & 0xF);
-      s.cov_kw = (uint32_t)(w1v >> 32);
-      s.cnt += (e >> 16) & 0x1FFF;
-      s.st = 0;
-    } else {
-      done = t;
-      break;
-    }
-    path |= 1ull << t;
-    if (lane == t) post = s;
-  }
-  // lanes off the path carry the state of the last path lane before them
-  // (or the incoming state, which every lane already holds in `post`)
-  const uint64_t below = path & ((lane == 63) ? ~0ull : ((2ull << lane) - 1));
-  const int src = below ? 63 - __builtin_clzll(below) : -1;
-  {
-    const int a = (src >= 0 ? src : (int)lane) * 4;
-    cstate q;
-    q.X = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(post.X >> 32)) << 32) |
-          (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)post.X);
-    q.cov_ps = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(post.cov_ps >> 32)) << 32) |
-               (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)post.cov_ps);
-    q.cov_start = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(post.cov_start >> 32)) << 32) |
-                  (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)post.cov_start);
-    q.cnt = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(post.cnt >> 32)) << 32) |
-            (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)post.cnt);
-    q.cov_kw = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)post.cov_kw);
-    q.st = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)post.st);
-    if (src >= 0) post = q;
-  }
-  return done;
-}
-
-// Lanes l < k publish their post-state as segment w0+l's inclusive record
-// (skipping segments already inclusive).
-XYWS_DEV void publish_window(const st_params& P, uint64_t w0, uint32_t k, uint32_t lane,
-                             const seg_view& v, const cstate& post) {
-  const bool mine = lane < k && v.f < F_INCL;
-  if (mine) {
-    uint64_t* r = P.recs + (w0 + lane) * R_WORDS;
-    st_store(r + R_INC + 0, post.X);
-    st_store(r + R_INC + 1, post.cov_ps);
-    st_store(r + R_INC + 2, post.cov_start);
-    st_store(r + R_INC + 3, (uint64_t)post.cov_kw | ((uint64_t)post.st << 32));
-    st_store(r + R_INC + 4, post.cnt);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (mine) __hip_atomic_store(P.flags + w0 + lane, F_INCL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-XYWS_DEV cstate wave_rec_incl(const st_params& P, int64_t j) {
-  if (j < 0) return initial_state(P);
-  return rec_incl(P.recs + (uint64_t)j * R_WORDS);
-}
-
-// Exact state before segment `seg`, computed by the whole wave (result uniform).
-XYWS_DEV cstate lookback_wave(const st_params& P, uint64_t seg, uint32_t lane) {
+// Step C: is the assumed input of segment k exact? It is when some earlier
+// segment a has an exact output and every segment j in (a, k] assumed exactly
+// its predecessor's published output (pair flag fP[j] = 1); when a's exact
+// output came from the slow path, segment a+1's input is compared with it
+// directly. A decoupled look-back over 64 flags per round trip: pair flags are
+// published from local work only, so nothing here waits on other validations.
+XYWS_DEV bool validate_wave(const st_params& P, uint64_t k, uint32_t lane) {
   uint32_t* err = P.head + 1;
-  if (seg == 0) return initial_state(P);
-  // nearest inclusive predecessor (j = -1: the batch start)
-  int64_t j = -1;
-  if (stat_on(P)) stat_add(P, ST_LB, 1);
-  for (int64_t b = (int64_t)seg - 1; b >= 0; b -= 64) {
-    const int64_t i = b - (int64_t)lane;
-    const uint32_t f = i >= 0 ? flag_load(P.flags + i) : F_INCL;
-    const uint64_t m = __ballot(f >= F_INCL);
-    if (m) { j = b - (int64_t)__builtin_ctzll(m); break; }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  cstate s = wave_rec_incl(P, j);
-  uint64_t w0 = (uint64_t)(j + 1);
-  for (uint32_t guard = 0; w0 < seg && guard < 1u << 20; guard++) {
-    const uint32_t n = seg - w0 < 64 ? (uint32_t)(seg - w0) : 64u;
-    seg_view v;
-    load_view(P, w0 + lane, lane < n, v);
-    cstate post = s;
-    const uint32_t k = compose_window(P, s, w0, n, v, lane, post);
-    publish_window(P, w0, k, lane, v, post);
-    if (stat_on(P)) { stat_add(P, ST_LB_WIN, 1); stat_add(P, ST_LB_SEG, k); }
-    w0 += k;
-    if (k < n) {  // segment w0 needs its own inclusive record (or its aggregate)
-      if (stat_on(P)) stat_add(P, ST_LB_STALL, 1);
-      // exact header chase through segment w0 in global memory (headers are
-      // immutable); only a long chase waits for the owner's inclusive record
-      bool inc = false;
-      cstate c = s;
-      chase_global(P, c, (w0 + 1) * SEG, 16, &inc);
-      if (!inc) {
-        s = c;
-        if (lane == 0) pub_incl(P, w0, s);
-        w0 += 1;
-        continue;
-      }
-      if (stat_on(P)) stat_add(P, ST_LB_WAITINC, 1);
-      if (!flag_wait(P.flags + w0, F_INCL, err)) { s.X = ~0ull; break; }
-      s = rec_incl(P.recs + w0 * R_WORDS);
-      w0 += 1;
+  for (int64_t b = (int64_t)k - 1, rounds = 0; rounds < 64; b -= 64, rounds++) {
+    const int64_t j = b - (int64_t)lane;
+    uint32_t fv = j >= 0 ? flag_load(P.fV + j) : (j == -1 ? 3u : 0u);
+    const uint64_t mv = __ballot(fv >= 1);
+    const uint32_t la = mv ? (uint32_t)__builtin_ctzll(mv) : 64u;
+    // pair flags of the segments after the anchor (k's own pair is lane -1: checked by caller)
+    uint32_t fp = (lane < la && j >= 0) ? flag_load(P.fP + j) : 1u;
+    for (uint32_t it = 0; !__all(fp != 0) && it < SPIN; it++) {
+      __builtin_amdgcn_s_sleep(1);
+      if (fp == 0) fp = flag_load(P.fP + j);
     }
+    if (!__all(fp != 0)) { atomicOr(err, 4u); return false; }
+    if (__ballot(fp == 2)) return false;
+    if (!mv) continue;  // all 64 pairs good, anchor further back
+    const uint32_t fva = rl32(fv, la);
+    if (fva == 2) {  // slow-path anchor: its successor must have assumed its exact output
+      const int64_t a = b - (int64_t)la;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const cstate E = exact_out(P, a, 2);
+      cstate In;
+      if ((uint64_t)(a + 1) == k) return true;  // caller compares k's own input with it
+      In = load_state(P.recs + (uint64_t)(a + 1) * R_WORDS + R_CI);
+      return same_state(In, E);
+    }
+    return true;
   }
-  return s;
+  return false;
 }
 
-// After resolving segment `seg` with exact output o: publish the inclusive
-// records of the successors the wave can compose from their aggregates.
-XYWS_DEV void help_wave(const st_params& P, uint64_t seg, cstate o, uint32_t lane) {
-  uint64_t w0 = seg + 1;
-  for (uint32_t round = 0; round < HELP / 64 && w0 < P.nseg; round++) {
-    const uint32_t n = P.nseg - w0 < 64 ? (uint32_t)(P.nseg - w0) : 64u;
-    seg_view v;
-    load_view(P, w0 + lane, lane < n, v);
-    // stop at segments already inclusive (someone else is ahead) or not yet aggregated
-    const uint64_t stop = __ballot(lane < n && (v.f < F_AGG || v.f >= F_INCL));
-    const uint32_t lim = stop ? (uint32_t)__builtin_ctzll(stop) : n;
-    cstate post = o;
-    const uint32_t k = compose_window(P, o, w0, lim, v, lane, post);
-    publish_window(P, w0, k, lane, v, post);
-    if (stat_on(P)) { stat_add(P, ST_HELP_WIN, 1); stat_add(P, ST_HELP_SEG, k); }
-    if (k < n) break;
-    w0 += n;
+// Step D: exclusive frame-count prefix of segment k (decoupled look-back sum).
+XYWS_DEV uint64_t count_prefix(const st_params& P, uint64_t k, uint32_t lane) {
+  uint32_t* err = P.head + 1;
+  uint64_t sum = 0;
+  int64_t b = (int64_t)k - 1;
+  for (uint32_t guard = 0; b >= 0 && guard < (1u << 20); guard++) {
+    const int64_t j = b - (int64_t)lane;
+    uint32_t fn = j >= 0 ? flag_load(P.fN + j) : 2u;
+    const uint64_t mi = __ballot(fn >= 2);
+    const uint32_t li = mi ? (uint32_t)__builtin_ctzll(mi) : 64u;
+    bool ready = lane >= li || fn >= 1;
+    for (uint32_t it = 0; !__all(ready) && it < SPIN; it++) {
+      __builtin_amdgcn_s_sleep(2);
+      if (!ready) { fn = flag_load(P.fN + j); ready = fn >= 1; }
+    }
+    if (!__all(ready)) { atomicOr(err, 8u); return sum; }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint64_t v = 0;
+    if (lane < li) v = st_load(P.recs + (uint64_t)j * R_WORDS + R_NA);
+    else if (lane == li && j >= 0) v = st_load(P.recs + (uint64_t)j * R_WORDS + R_NI);
+#pragma unroll
+    for (uint32_t o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);  // lanes > li hold 0
+    sum += v;
+    if (mi) break;
+    b -= 64;
   }
+  return sum;
+}
+
+// The exact frames of segment k from input s (lane 0): the suffix of a primary
+// walk of the survivor graph (mode 1), or an exact header chase (mode 2).
+struct chain_res {
+  cstate o;
+  uint32_t mode, ordx, outx, npre;
+};
+
+XYWS_DEV chain_res own_chain(const st_params& P, st_lds& L, uint32_t nsurv, uint64_t ss,
+                             uint64_t se, const cstate& s) {
+  chain_res c;
+  c.o = s; c.mode = 0; c.ordx = 0; c.outx = 0; c.npre = 0;
+  if ((s.st & S_PARTIAL) || s.X >= se || s.X >= P.hi) return c;
+  const uint32_t xr = (uint32_t)(s.X - ss);
+  uint32_t x = 0, y = nsurv;
+  while (x < y) {
+    const uint32_t m = (x + y) >> 1;
+    if (L.s_pos[m] < xr) x = m + 1; else y = m;
+  }
+  bool hit = x < nsurv && L.s_pos[x] == xr && L.s_out[x] < NOUT;
+  uint32_t npre = 0;
+  if (hit) {  // non-primary entry: walk its prefix up to the primary walk it joins
+    uint32_t kk = x;
+    while (L.s_ord[kk] == ORD_NONE && npre < 64) { L.s_ord_pre[npre++] = (uint16_t)kk; kk = L.s_nxt[kk]; }
+    if (L.s_ord[kk] == ORD_NONE) hit = false;
+    else x = kk;
+  }
+  if (hit) {
+    c.mode = 1;
+    c.ordx = L.s_ord[x];
+    c.outx = L.s_out[x];
+    c.npre = npre;
+    c.o.X = L.outs[c.outx][0]; c.o.cov_ps = L.outs[c.outx][1]; c.o.cov_start = L.outs[c.outx][2];
+    c.o.cov_kw = (uint32_t)L.outs[c.outx][3];
+    c.o.cnt = s.cnt + L.s_rem[x] + npre;
+    c.o.st = 0;
+  } else {
+    c.mode = 2;
+    bool inc = false;
+    chase_global(P, c.o, se, 0xFFFFFFFFu, &inc);
+  }
+  return c;
 }
 
 XYWS_DEV void write_frame(const st_params& P, uint64_t ord, uint64_t start, const hdr_info& h,
@@ -825,67 +883,127 @@ __global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
           st_store(rec + R_OUT0 + 2 * o + 1, (outs[o][1] - ss) | ((outs[o][1] - outs[o][2]) << 20) |
                                                  (outs[o][3] << 32));
         }
-        flag_publish(P.flags + seg, F_AGG);
+        flag_publish(P.fA + seg, 1u);
       }
 
-      // ---- 4. look-back (whole wave): exact state before this segment
-      cstate s = lookback_wave(P, seg, lane);
+      // ---- 4. input state: exact, or speculated from the aggregates (wave)
+      bool exact = false;
+      cstate I = resolve_input(P, L, seg, lane, exact);
+      const bool spec = !exact && !(I.st & S_NONE);
+      uint64_t* rec = P.recs + seg * R_WORDS;
 
-      // ---- 5a. own exact chain (lane 0): primary-walk suffix or exact chase
-      cstate o = s;
+      // ---- 5a. own frames from that input (lane 0); publish (input, output)
+      chain_res c;
       if (lane == 0) {
-        uint32_t mode = 0, ordx = 0, outx = 0, npre = 0;
-        if (!(s.st & S_PARTIAL) && s.X < se && s.X < hi) {
-          const uint32_t xr = (uint32_t)(s.X - ss);
-          uint32_t x = 0, y = nsurv;
-          while (x < y) {
-            const uint32_t m = (x + y) >> 1;
-            if (L.s_pos[m] < xr) x = m + 1; else y = m;
-          }
-          bool hit = x < nsurv && L.s_pos[x] == xr && L.s_out[x] < NOUT;
-          if (hit) {  // non-primary entry: walk its prefix up to the primary walk it joins
-            uint32_t k = x;
-            while (L.s_ord[k] == ORD_NONE && npre < 64) { L.s_ord_pre[npre++] = (uint16_t)k; k = L.s_nxt[k]; }
-            if (L.s_ord[k] == ORD_NONE) hit = false;
-            else x = k;
-          }
-          if (hit) {
-            mode = 1;
-            ordx = L.s_ord[x];
-            outx = L.s_out[x];
-            o.X = L.outs[outx][0]; o.cov_ps = L.outs[outx][1]; o.cov_start = L.outs[outx][2];
-            o.cov_kw = (uint32_t)L.outs[outx][3];
-            o.cnt = s.cnt + L.s_rem[x] + npre;
-            o.st = 0;
-          } else {
-            mode = 2;
-            npre = 0;
-            bool inc = false;
-            chase_global(P, o, se, 0xFFFFFFFFu, &inc);
+        if (exact || spec) {
+          c = own_chain(P, L, nsurv, ss, se, I);
+          store_state(rec + R_CI, I);
+          store_state(rec + R_CO, c.o);
+          st_store(rec + R_CN, c.o.cnt);
+          flag_publish(P.fC + seg, 1u);
+          if (exact) flag_publish(P.fV + seg, 1u);
+        } else {
+          c.mode = 0;  // placeholder: resolved by the slow path below
+        }
+      }
+      if (stat_on(P)) stat_add(P, exact ? ST_EXACT_IN : spec ? ST_SPEC : ST_NOSPEC, 1);
+
+      // ---- 5b. own pair flag: assumed input == predecessor's published output
+      bool ok = exact;
+      if (spec) {
+        uint32_t fc = 0;
+        for (uint32_t it = 0; it < SPIN; it++) {
+          fc = flag_load(P.fC + seg - 1);
+          if (fc >= 1) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const cstate Op = load_state(P.recs + (seg - 1) * R_WORDS + R_CO);
+        const bool pair = fc >= 1 && same_state(I, Op);
+        if (lane == 0) flag_publish(P.fP + seg, pair ? 1u : 2u);
+        // ---- 5c. validation (wave): pair flags back to an exact segment
+        if (pair) {
+          ok = validate_wave(P, seg, lane);
+          if (ok) {  // a slow-path predecessor anchor: compare with its exact output
+            const uint32_t fvp = flag_load(P.fV + seg - 1);
+            if (fvp == 2) ok = same_state(I, exact_out(P, (int64_t)seg - 1, 2));
           }
         }
-        L.in = s;
-        L.out = o;
-        L.mode = mode;
-        L.ord_x = ordx;
-        L.out_x = outx;
-        L.npre = npre;
-        pub_incl(P, seg, o);
+      } else if (lane == 0) {
+        flag_publish(P.fP + seg, exact ? 1u : 2u);
+      }
+      // otherwise wait for the predecessor's exact output (slow path)
+      if (!ok) {
+        if (stat_on(P)) stat_add(P, ST_SLOW, 1);
+        uint32_t fvp = 0;
+        for (uint32_t it = 0; it < SPIN; it++) {
+          fvp = flag_load(P.fV + seg - 1);
+          if (fvp >= 1) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (fvp == 0) atomicOr(P.head + 1, 16u);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        cstate E = exact_out(P, (int64_t)seg - 1, fvp);
+        E.cnt = 0;
+        if (spec && same_state(E, I)) {
+          ok = true;  // the speculation was right after all
+          if (lane == 0) flag_publish(P.fV + seg, 1u);
+        } else {
+          if (stat_on(P)) stat_add(P, ST_RECOMP, 1);
+          I = E;
+          if (lane == 0) {
+            c = own_chain(P, L, nsurv, ss, se, I);
+            if (!spec) {  // nothing published yet: the exact pair serves the validators
+              store_state(rec + R_CI, I);
+              store_state(rec + R_CO, c.o);
+              st_store(rec + R_CN, c.o.cnt);
+              flag_publish(P.fC + seg, 1u);
+            }
+            store_state(rec + R_EX, c.o);
+            st_store(rec + R_EN, c.o.cnt);
+            flag_publish(P.fV + seg, 2u);
+          }
+        }
+      } else if (spec && lane == 0) {
+        flag_publish(P.fV + seg, 1u);
+      }
+      if (stat_on(P) && ok && spec) stat_add(P, ST_VALID, 1);
+
+      // ---- 5c. frame count: aggregate + prefix (only ordinals need it) ------
+      uint64_t n = rl64(lane == 0 ? c.o.cnt : 0, 0);
+      if (lane == 0) {
+        st_store(rec + R_NA, n);
+        flag_publish(P.fN + seg, 1u);
+        atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 4), (unsigned long long)n);
+      }
+      uint64_t nbase = 0;
+      if (P.frames) {
+        nbase = count_prefix(P, seg, lane);
+        if (lane == 0) {
+          st_store(rec + R_NI, nbase + n);
+          flag_publish(P.fN + seg, 2u);
+        }
+      }
+      if (lane == 0) {
+        L.in = I;
+        L.out = c.o;
+        L.mode = c.mode;
+        L.ord_x = c.ordx;
+        L.out_x = c.outx;
+        L.npre = c.npre;
+        L.nbase = nbase;
         if (stat_on(P)) {
-          stat_add(P, mode == 2 ? ST_MODE2 : ST_MODE1, 1);
+          stat_add(P, c.mode == 2 ? ST_MODE2 : ST_MODE1, 1);
           stat_add(P, ST_NSURV, nsurv);
         }
       }
-      o = bcast_state(o);  // lane 0's result to the wave
-
-      // ---- helping (whole wave): carry the exact state through successors
-      help_wave(P, seg, o, lane);
     }
     __syncthreads();
 
     // ---- 5b/6. frame-list passes, XOR into registers -------------------------
     const cstate sin = L.in;
     const uint32_t mode = L.mode;
+    const uint64_t fb = L.nbase + sin.cnt;  // ordinal of the first frame starting in this segment
     uint32_t changed = 0;
 
     // the carried-header frame of the batch is described by segment 0
@@ -904,7 +1022,7 @@ __global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
         L.flist[0] = e;
         L.nfl = 1;
       }
-      L.fbase = sin.cnt;
+      L.fbase = fb;
       L.chase_X = sin.X;
       L.pass_done = (mode != 2);
     }
@@ -923,11 +1041,11 @@ __global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
         L.flist[L.nfl + tid] = e;
         if (P.frames) {
           hdr_info hh = header_global(P.base, p, hi);
-          write_frame(P, sin.cnt + tid, p, hh, ps, 0);
+          write_frame(P, fb + tid, p, hh, ps, 0);
         }
       }
       const uint32_t base_n = L.nfl + npre;
-      const uint64_t cbase = sin.cnt + npre;
+      const uint64_t cbase = fb + npre;
       uint32_t cnt = 0;
       for (uint32_t i = tid; i < nsurv; i += NT) {
         const uint16_t od = L.s_ord[i];
@@ -1022,42 +1140,46 @@ __global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
       }
     }
 
-    // ---- last segment: frame count + carry out --------------------------------
-    if (seg == P.nseg - 1 && tid == 0) {
-      const cstate o = L.out;
-      if (P.nframes) *P.nframes = o.cnt;
-      if (P.cout) {
-        xyws_carry c;
-        for (int i = 0; i < 64; i++) reinterpret_cast<uint8_t*>(&c)[i] = 0;
-        c.frames_total = P.cin->frames_total + o.cnt;
-        if (o.st & S_PARTIAL) {
-          uint32_t n = 0;
-          if (o.st & S_PARTCARRY) {
-            for (; n < P.cin->hdr_len; n++) c.hdr[n] = P.cin->hdr[n];
-            for (uint64_t q = lo; q < hi && n < 14; q++) c.hdr[n++] = P.base[q];
-          } else {
-            for (uint64_t q = o.X; q < hi && n < 14; q++) c.hdr[n++] = P.base[q];
-          }
-          c.hdr_len = (uint8_t)n;
-        } else if (o.X > hi && !(o.st & S_NOCOV)) {
-          if (o.st & S_CARRIED) {
-            c.payload_remaining = P.cin->payload_remaining - (hi - lo);
-            c.phase = P.cin->phase + (hi - lo);
-            for (int i = 0; i < 4; i++) c.key[i] = P.cin->key[i];
-          } else {
-            hdr_info hh;
-            if (o.st & S_HDRCARRY) {
-              hh = header_carried(P.base, lo, hi, P.cin);
+    // ---- the last workgroup to finish: frame count + carry out -------------
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const uint32_t done = atomicAdd(P.head + 2, 1u);
+      if (done == P.nseg - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const uint64_t total = __hip_atomic_load(reinterpret_cast<uint64_t*>(P.head + 4),
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t fvl = flag_load(P.fV + P.nseg - 1);
+        const cstate o = exact_out(P, (int64_t)P.nseg - 1, fvl);
+        if (P.nframes) *P.nframes = total;
+        if (P.cout) {
+          xyws_carry c;
+          for (int i = 0; i < 64; i++) reinterpret_cast<uint8_t*>(&c)[i] = 0;
+          c.frames_total = P.cin->frames_total + total;
+          if (o.st & S_PARTIAL) {
+            uint32_t nb = 0;
+            if (o.st & S_PARTCARRY) {
+              for (; nb < P.cin->hdr_len; nb++) c.hdr[nb] = P.cin->hdr[nb];
+              for (uint64_t q = lo; q < hi && nb < 14; q++) c.hdr[nb++] = P.base[q];
             } else {
-              hh = header_global(P.base, o.cov_start, hi);
+              for (uint64_t q = o.X; q < hi && nb < 14; q++) c.hdr[nb++] = P.base[q];
             }
-            c.payload_remaining = hh.plen - (hi - o.cov_ps);
-            c.phase = hi - o.cov_ps;
-            c.key[0] = (uint8_t)hh.key; c.key[1] = (uint8_t)(hh.key >> 8);
-            c.key[2] = (uint8_t)(hh.key >> 16); c.key[3] = (uint8_t)(hh.key >> 24);
+            c.hdr_len = (uint8_t)nb;
+          } else if (o.X > hi && !(o.st & S_NOCOV)) {
+            if (o.st & S_CARRIED) {
+              c.payload_remaining = P.cin->payload_remaining - (hi - lo);
+              c.phase = P.cin->phase + (hi - lo);
+              for (int i = 0; i < 4; i++) c.key[i] = P.cin->key[i];
+            } else {
+              const hdr_info hh = (o.st & S_HDRCARRY) ? header_carried(P.base, lo, hi, P.cin)
+                                                      : header_global(P.base, o.cov_start, hi);
+              c.payload_remaining = hh.plen - (hi - o.cov_ps);
+              c.phase = hi - o.cov_ps;
+              c.key[0] = (uint8_t)hh.key; c.key[1] = (uint8_t)(hh.key >> 8);
+              c.key[2] = (uint8_t)(hh.key >> 16); c.key[3] = (uint8_t)(hh.key >> 24);
+            }
           }
+          *P.cout = c;
         }
-        *P.cout = c;
       }
     }
     __syncthreads();
@@ -1106,7 +1228,7 @@ void stream_scratch_free(stream_scratch* s) {
   s->max_tiles = 0;
 }
 
-static uint64_t flags_bytes(uint64_t n) { return (n * 4 + 255) & ~255ull; }
+static uint64_t flags_bytes(uint64_t n) { return (5 * n * 4 + 255) & ~255ull; }  // fA fC fV fN fP
 
 static int scratch_grow(stream_scratch* s, uint64_t segs) {
   if (s->mem && segs <= s->max_tiles) return XYWS_OK;
@@ -1162,7 +1284,12 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   P.base = base; P.lo = lo; P.hi = hi; P.nseg = nseg;
   P.cout = cout; P.frames = frames; P.cap = cap; P.nframes = nframes;
   P.head = reinterpret_cast<uint32_t*>(m);
-  P.flags = reinterpret_cast<uint32_t*>(m + HEAD_BYTES);
+  uint32_t* fl = reinterpret_cast<uint32_t*>(m + HEAD_BYTES);
+  P.fA = fl;
+  P.fC = fl + nseg;
+  P.fV = fl + 2 * nseg;
+  P.fN = fl + 3 * nseg;
+  P.fP = fl + 4 * nseg;
   P.recs = reinterpret_cast<uint64_t*>(m + HEAD_BYTES + flags_bytes(s->max_tiles));
   P.opts = opts;
   // Ticket + flags zeroed every call (the error word [1] is sticky until read
@@ -1170,6 +1297,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   // dev_carry_out, which the last segment writes while others may still read
   // the incoming carry.
   xyws_carry* snap = reinterpret_cast<xyws_carry*>(m + 64);
+  if (hipMemsetAsync(P.head + 2, 0, 24, stream) != hipSuccess) return XYWS_ERR_HIP;  // done, total
   if (hipMemsetAsync(P.head, 0, 4, stream) != hipSuccess) return XYWS_ERR_HIP;
   if ((opts & XYWS_OPT_STATS) && hipMemsetAsync(m + 128, 0, 128, stream) != hipSuccess) return XYWS_ERR_HIP;
   if (cin) {
@@ -1179,7 +1307,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     return XYWS_ERR_HIP;
   }
   P.cin = snap;
-  if (hipMemsetAsync(P.flags, 0, (nseg * 4 + 15) & ~15ull, stream) != hipSuccess) return XYWS_ERR_HIP;
+  if (hipMemsetAsync(fl, 0, (5 * nseg * 4 + 15) & ~15ull, stream) != hipSuccess) return XYWS_ERR_HIP;
   int grid = occupancy_grid();
   if ((uint64_t)grid > nseg) grid = (int)nseg;
   hipLaunchKernelGGL(k_stream_fused, dim3(grid), dim3(NT), 0, stream, P);
