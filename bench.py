@@ -239,14 +239,21 @@ def main():
 
     if args.stats and rank == 0:  # one extra counted decode pair (keeps the step parity)
         names = ["exact_in", "spec", "no_spec", "valid", "slow", "recomputed", "no_anchor",
-                 "mode1", "mode2", "survivors", "spins"]
+                 "mode1", "mode2", "survivors", "spins", "-", "-", "-", "-", "-",
+                 "cyc_pass1", "cyc_walk", "cyc_input", "cyc_chain", "cyc_valid", "cyc_count",
+                 "cyc_xor", "cyc_store"]
         for _ in range(2):
             dec.opts |= 0x100
             dec.decode(buf, cap=0, count=False, carry=False)
             dec.opts &= ~0x100
-            out = (C.c_uint64 * 16)()
+            out = (C.c_uint64 * 32)()
             dec.ctx.L.xyws_debug_stats(dec.ctx.h, out)
-        print(json.dumps({"stats": dict(zip(names, list(out)[:len(names)]))}), flush=True)
+        st = {k: v for k, v in zip(names, list(out)) if k != "-"}
+        nseg = max(1, st["mode1"] + st["mode2"])
+        for k in list(st):
+            if k.startswith("cyc_"):
+                st[k.replace("cyc_", "us_per_seg_")] = round(st.pop(k) / nseg / 2100.0, 3)
+        print(json.dumps({"stats": st}), flush=True)
 
     # parity after the timed region: total decodes = warmup + steps
     dev_err = dec.ctx.last_device_error()

@@ -415,7 +415,7 @@ int xyws_ctx_last_device_error(xyws_ctx* ctx, uint32_t* out) {
 
 // Internal (not part of include/xyws.h): resolution counters of the last fused
 // stream decode run with XYWS_OPT_STATS (0x100). Synchronizes the device.
-int xyws_debug_stats(xyws_ctx* ctx, uint64_t out[16]) {
+int xyws_debug_stats(xyws_ctx* ctx, uint64_t out[32]) {
   if (!ctx || !out) return XYWS_ERR_INVALID;
   device_guard g(ctx->device);
   return stream_scratch_stats(&ctx->ss, out);

@@ -16,7 +16,7 @@ void stream_scratch_init(stream_scratch* s);
 void stream_scratch_free(stream_scratch* s);
 int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes);
 uint32_t stream_scratch_error(stream_scratch* s);
-int stream_scratch_stats(stream_scratch* s, uint64_t out[16]);
+int stream_scratch_stats(stream_scratch* s, uint64_t out[32]);
 
 // Internal decode option: count resolution events (xyws_debug_stats).
 #define XYWS_OPT_STATS 0x100u  // synchronous read of the error word

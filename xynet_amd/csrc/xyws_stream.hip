@@ -70,7 +70,8 @@ constexpr uint32_t NT = 256;             // threads per workgroup
 constexpr uint32_t CHS = SEG / (16 * NT);  // 32 chunks per lane
 constexpr uint32_t CHSUB = SUB / (16 * NT);  // 8 chunks per lane per sub-tile
 constexpr uint32_t HALO = 16;
-constexpr uint32_t SMAX = 1024;          // survivors tracked per segment
+constexpr uint32_t SMAX = 512;           // survivors tracked per segment
+constexpr uint32_t LV = 9;               // jump-table levels: 2^LV >= SMAX
 constexpr uint32_t FCAP = SUB / 16;      // frame-list entries per pass (overlays the sub-tile)
 constexpr uint32_t NENT = 16;            // aggregate entry nodes (2 per record word)
 constexpr uint32_t NOUT = 8;             // aggregate outcomes (2 record words each)
@@ -79,8 +80,9 @@ constexpr uint32_t SPIN = 1u << 24;      // bounded spins (~1 s)
 constexpr uint32_t WIN = 64;             // segments seen by one look-back (one per lane)
 constexpr uint32_t BKT = 8;              // exits kept per target segment during speculation
 constexpr uint16_t N_EXIT = 0xFFFF, N_DEAD = 0xFFFE;
-constexpr uint8_t O_NONE = 0xFF, O_DEAD = 0xFE, O_UNREC = 0xFD;  // node outcome marks
-constexpr uint16_t ORD_NONE = 0xFFFF;
+constexpr uint8_t O_DEAD = 0xFE, O_UNREC = 0xFD;  // node outcome marks
+constexpr uint16_t J_TERM = 0xFFFF;      // jump past the end of a chain
+constexpr uint16_t T_DEAD = 0xFFFF;      // chain ends in a dead end
 
 // composition-state bits
 constexpr uint32_t S_PARTIAL = 1;    // stream ended in an incomplete header at X
@@ -128,8 +130,9 @@ struct __attribute__((aligned(16))) st_lds {
   uint32_t s_nrel[SMAX];      // successor position (segment-relative, saturating)
   uint32_t s_key[SMAX];
   uint16_t s_nxt[SMAX];       // successor survivor index / N_EXIT / N_DEAD
-  uint16_t s_rem[SMAX];       // frames from this node to the exit
-  uint16_t s_ord[SMAX];       // ordinal on the primary walk of its outcome
+  uint16_t s_jmp[LV][SMAX];   // s_jmp[b][i]: the 2^b-th successor of i (J_TERM past the chain end)
+  uint16_t s_rem[SMAX];       // frames from this node to the chain end
+  uint16_t s_last[SMAX];      // last node of the chain (T_DEAD: ends in a dead end)
   uint8_t s_out[SMAX];        // outcome id / O_* mark
   uint8_t s_hlen[SMAX];
   uint32_t scan[8];
@@ -138,8 +141,7 @@ struct __attribute__((aligned(16))) st_lds {
   uint32_t nsurv, overflow, nfl, pass_done;
   cstate in, out;
   uint64_t chase_X, fbase;
-  uint32_t mode, ord_x, out_x, npre;
-  uint16_t s_ord_pre[64];     // non-primary prefix of the entry's path
+  uint32_t mode, node_x, rem_x, nent_pub, nout_pub, more_j;
   uint64_t outs[NOUT][4];     // aggregate outcomes: exit, cov_ps, cov_start, kw
   uint32_t ents[NENT];        // aggregate entries (packed as in the record)
   uint32_t bk_n[WIN];         // speculation: exits landing in each window segment
@@ -169,7 +171,9 @@ struct st_params {
 // With XYWS_OPT_STATS the kernel counts resolution events into head[16..32)
 // (read back by xyws_debug_stats). Off by default: one uniform branch each.
 enum { ST_EXACT_IN = 0, ST_SPEC, ST_NOSPEC, ST_VALID, ST_SLOW, ST_RECOMP, ST_NOANCHOR,
-       ST_MODE1, ST_MODE2, ST_NSURV, ST_SPINS, ST_NSTAT = 16 };
+       ST_MODE1, ST_MODE2, ST_NSURV, ST_SPINS,
+       ST_T_PASS1 = 16, ST_T_WALK, ST_T_INPUT, ST_T_CHAIN, ST_T_VALID, ST_T_COUNT, ST_T_XOR, ST_T_STORE,
+       ST_NSTAT = 32 };
 
 // ---------------------------------------------------------------- hand-off
 XYWS_DEV void st_store(uint64_t* p, uint64_t v) {
@@ -190,6 +194,15 @@ XYWS_DEV void stat_add(const st_params& P, uint32_t i, uint64_t v) {
   if (__builtin_amdgcn_mbcnt_lo(~0u, 0) == 0)  // one lane
     atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + i, (unsigned long long)v);
 }
+// Per-phase cycle accounting (stats builds only): adds now - *t to slot i.
+XYWS_DEV void stat_phase(const st_params& P, uint32_t i, uint64_t& t) {
+  if (!stat_on(P)) return;
+  const uint64_t now = __builtin_amdgcn_s_memtime();
+  stat_add(P, i, now - t);
+  t = now;
+}
+
+XYWS_DEV bool wid0(uint32_t wave) { return wave == 0; }
 
 XYWS_DEV bool flag_wait(const uint32_t* p, uint32_t want, uint32_t* err) {
   for (uint32_t it = 0; it < SPIN; it++) {
@@ -584,13 +597,13 @@ XYWS_DEV uint64_t count_prefix(const st_params& P, uint64_t k, uint32_t lane) {
 // walk of the survivor graph (mode 1), or an exact header chase (mode 2).
 struct chain_res {
   cstate o;
-  uint32_t mode, ordx, outx, npre;
+  uint32_t mode, node, rem;  // mode 1: the path from survivor `node`, rem frames
 };
 
 XYWS_DEV chain_res own_chain(const st_params& P, st_lds& L, uint32_t nsurv, uint64_t ss,
                              uint64_t se, const cstate& s) {
   chain_res c;
-  c.o = s; c.mode = 0; c.ordx = 0; c.outx = 0; c.npre = 0;
+  c.o = s; c.mode = 0; c.node = 0; c.rem = 0;
   if ((s.st & S_PARTIAL) || s.X >= se || s.X >= P.hi) return c;
   const uint32_t xr = (uint32_t)(s.X - ss);
   uint32_t x = 0, y = nsurv;
@@ -598,22 +611,14 @@ XYWS_DEV chain_res own_chain(const st_params& P, st_lds& L, uint32_t nsurv, uint
     const uint32_t m = (x + y) >> 1;
     if (L.s_pos[m] < xr) x = m + 1; else y = m;
   }
-  bool hit = x < nsurv && L.s_pos[x] == xr && L.s_out[x] < NOUT;
-  uint32_t npre = 0;
-  if (hit) {  // non-primary entry: walk its prefix up to the primary walk it joins
-    uint32_t kk = x;
-    while (L.s_ord[kk] == ORD_NONE && npre < 64) { L.s_ord_pre[npre++] = (uint16_t)kk; kk = L.s_nxt[kk]; }
-    if (L.s_ord[kk] == ORD_NONE) hit = false;
-    else x = kk;
-  }
-  if (hit) {
+  if (x < nsurv && L.s_pos[x] == xr && L.s_out[x] < NOUT) {
+    const uint32_t oc = L.s_out[x];
     c.mode = 1;
-    c.ordx = L.s_ord[x];
-    c.outx = L.s_out[x];
-    c.npre = npre;
-    c.o.X = L.outs[c.outx][0]; c.o.cov_ps = L.outs[c.outx][1]; c.o.cov_start = L.outs[c.outx][2];
-    c.o.cov_kw = (uint32_t)L.outs[c.outx][3];
-    c.o.cnt = s.cnt + L.s_rem[x] + npre;
+    c.node = x;
+    c.rem = L.s_rem[x];
+    c.o.X = L.outs[oc][0]; c.o.cov_ps = L.outs[oc][1]; c.o.cov_start = L.outs[oc][2];
+    c.o.cov_kw = (uint32_t)L.outs[oc][3];
+    c.o.cnt = s.cnt + c.rem;
     c.o.st = 0;
   } else {
     c.mode = 2;
@@ -621,6 +626,28 @@ XYWS_DEV chain_res own_chain(const st_params& P, st_lds& L, uint32_t nsurv, uint
     chase_global(P, c.o, se, 0xFFFFFFFFu, &inc);
   }
   return c;
+}
+
+// Block-wide exclusive scan of one value per thread (all threads call).
+XYWS_DEV uint32_t block_scan(st_lds& L, uint32_t v, uint32_t lane, uint32_t wave, uint32_t& total) {
+  uint32_t x = v;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  __syncthreads();
+  if (lane == 63) L.scan[wave] = x;
+  __syncthreads();
+  uint32_t wb = 0, tot = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; i++) {
+    const uint32_t si = L.scan[i];
+    if (i < wave) wb += si;
+    tot += si;
+  }
+  total = tot;
+  return wb + x - v;
 }
 
 XYWS_DEV void write_frame(const st_params& P, uint64_t ord, uint64_t start, const hdr_info& h,
@@ -677,6 +704,7 @@ __global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
     __syncthreads();
     const uint64_t seg = L.seg_id;
     if (seg >= P.nseg) break;
+    uint64_t tstamp = stat_on(P) ? __builtin_amdgcn_s_memtime() : 0;
     const uint64_t ss = seg * SEG, se = ss + SEG;
 
     // ---- 1. loads: the whole segment into registers -----------------------
@@ -820,75 +848,138 @@ __global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
         nn = (x < nsurv && L.s_pos[x] == nr) ? (uint16_t)x : N_DEAD;
       }
       L.s_nxt[i] = nn;
-      L.s_out[i] = O_NONE;
-      L.s_ord[i] = ORD_NONE;
+      L.s_jmp[0][i] = (nn == N_EXIT || nn == N_DEAD) ? J_TERM : nn;
+      L.s_rem[i] = 1;
+      L.s_last[i] = nn == N_EXIT ? (uint16_t)i : (nn == N_DEAD ? T_DEAD : 0);
+    }
+    __syncthreads();
+
+    // ---- 2a. pointer doubling over the survivor graph (all threads) --------
+    // After round b, s_jmp[b][i] is the 2^b-th successor of i; s_rem and
+    // s_last converge to the frames to the chain end and its last node.
+    for (uint32_t b = 0; b + 1 < LV; b++) {
+      uint32_t nj[2], nr[2], nl[2];
+      bool any = false;
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t i = tid + h * NT;
+        nj[h] = J_TERM; nr[h] = 0; nl[h] = 0;
+        if (i < nsurv) {
+          const uint32_t j = L.s_jmp[b][i];
+          nr[h] = L.s_rem[i];
+          nl[h] = L.s_last[i];
+          if (j != J_TERM) {
+            const uint32_t jj = L.s_jmp[b][j];
+            nj[h] = jj;
+            nr[h] += L.s_rem[j];
+            if (jj == J_TERM) nl[h] = L.s_last[j];
+            any = true;
+          }
+        }
+      }
+      const bool more = __syncthreads_or(any);
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t i = tid + h * NT;
+        if (i < nsurv) {
+          L.s_jmp[b + 1][i] = (uint16_t)nj[h];
+          L.s_rem[i] = (uint16_t)nr[h];
+          L.s_last[i] = (uint16_t)nl[h];
+        }
+      }
+      __syncthreads();
+      if (!more) {  // every chain resolved: the remaining levels are all J_TERM
+        for (uint32_t bb = b + 2; bb < LV; bb++)
+          for (uint32_t i = tid; i < nsurv; i += NT) L.s_jmp[bb][i] = J_TERM;
+        break;
+      }
+    }
+    // outcome ids: chain-end nodes ranked in position order
+    {
+      uint32_t isl[2];
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t i = 2 * tid + h;
+        isl[h] = (i < nsurv && L.s_nxt[i] == N_EXIT) ? 1u : 0u;
+      }
+      uint32_t tot;
+      const uint32_t r0 = block_scan(L, isl[0] + isl[1], lane, wave, tot);
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t i = 2 * tid + h;
+        if (isl[h]) {
+          const uint32_t id = r0 + (h ? isl[0] : 0);
+          L.s_out[i] = id < NOUT ? (uint8_t)id : O_UNREC;
+          if (id < NOUT) {
+            const uint64_t pp = ss + L.s_pos[i];
+            const uint64_t ps = pp + L.s_hlen[i];
+            L.outs[id][0] = L.s_nrel[i] == 0xFFFFFFFFu ? ~0ull : ss + L.s_nrel[i];
+            L.outs[id][1] = ps;
+            L.outs[id][2] = pp;
+            L.outs[id][3] = aligned_key(L.s_key[i], ps, 0);
+          }
+        }
+      }
+      if (tid == 0) L.nout_pub = tot < NOUT ? tot : NOUT;
+      __syncthreads();
+      // every node's outcome = its chain end's; entries = the first NENT exiting nodes
+      uint32_t ex[2];
+      uint8_t oc[2];
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t i = 2 * tid + h;
+        oc[h] = O_DEAD;
+        if (i < nsurv) {
+          const uint32_t t = L.s_last[i];
+          oc[h] = t == T_DEAD ? O_DEAD : L.s_out[t];
+        }
+        ex[h] = oc[h] < NOUT ? 1u : 0u;
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t i = 2 * tid + h;
+        if (i < nsurv) L.s_out[i] = oc[h];
+      }
+      const uint32_t e0 = block_scan(L, ex[0] + ex[1], lane, wave, tot);
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        const uint32_t i = 2 * tid + h;
+        const uint32_t q = e0 + (h ? ex[0] : 0);
+        if (ex[h] && q < NENT) L.ents[q] = L.s_pos[i] | ((uint32_t)L.s_rem[i] << 16) | ((uint32_t)oc[h] << 29);
+      }
+      if (tid == 0) L.nent_pub = tot < NENT ? tot : NENT;
     }
     __syncthreads();
 
     // ---- 2b/3/4/5a: wave 0: graph walk + aggregate (lane 0), look-back
     //      (wave), own resolution (lane 0), helping (wave) ------------------------
+    if (wid0(wave)) stat_phase(P, ST_T_PASS1, tstamp);
     if (wave == 0) {
-      if (lane == 0) {
+      {  // publish the aggregate: lanes store words in parallel, one drain, one flag
         uint64_t* rec = P.recs + seg * R_WORDS;
-        uint32_t nout = 0, nent = 0;
-        uint64_t (&outs)[NOUT][4] = L.outs;
-        uint32_t (&ents)[NENT] = L.ents;
-        // memoized walk in position order
-        for (uint32_t i = 0; i < nsurv; i++) {
-          if (L.s_out[i] != O_NONE) continue;
-          uint32_t j = i, steps = 0;
-          uint8_t oc;
-          uint32_t remj = 0;
-          for (;;) {  // to the first node with a known outcome, the exit or a dead end
-            steps++;
-            const uint16_t n = L.s_nxt[j];
-            if (n == N_EXIT) {
-              if (nout < NOUT) {
-                const uint64_t p = ss + L.s_pos[j];
-                const uint64_t ps = p + L.s_hlen[j];
-                outs[nout][0] = L.s_nrel[j] == 0xFFFFFFFFu ? ~0ull : ss + L.s_nrel[j];
-                outs[nout][1] = ps;
-                outs[nout][2] = p;
-                outs[nout][3] = aligned_key(L.s_key[j], ps, 0);
-                oc = (uint8_t)nout++;
-              } else {
-                oc = O_UNREC;
-              }
-              remj = 0;
-              j = 0xFFFFFFFFu;
-              break;
-            }
-            if (n == N_DEAD) { oc = O_DEAD; j = 0xFFFFFFFFu; break; }
-            if (L.s_out[n] != O_NONE) { oc = L.s_out[n]; remj = L.s_rem[n]; j = n; break; }
-            j = n;
-          }
-          // second walk: outcome, remaining count, primary ordinals
-          const bool primary = (oc < NOUT) && (j == 0xFFFFFFFFu);
-          uint32_t k = i;
-          for (uint32_t q = 0; q < steps; q++) {
-            L.s_out[k] = oc;
-            L.s_rem[k] = (uint16_t)(steps - q + remj);
-            if (primary) L.s_ord[k] = (uint16_t)q;
-            if (oc < NOUT && nent < NENT)
-              ents[nent++] = L.s_pos[k] | ((steps - q + remj) << 16) | ((uint32_t)oc << 29);
-            k = L.s_nxt[k];
-          }
+        const uint32_t nent = L.nent_pub, nout = L.nout_pub;
+        if (lane == 0)
+          st_store(rec + R_META, (uint64_t)nent | ((uint64_t)nout << 8) | ((uint64_t)L.overflow << 16));
+        if (lane < (nent + 1) / 2) {
+          const uint32_t q = 2 * lane;
+          st_store(rec + R_ENT0 + lane, (uint64_t)L.ents[q] | (q + 1 < nent ? (uint64_t)L.ents[q + 1] << 32 : 0));
         }
-        // publish the aggregate
-        st_store(rec + R_META, (uint64_t)nent | ((uint64_t)nout << 8) | ((uint64_t)L.overflow << 16));
-        for (uint32_t q = 0; q < nent; q += 2)
-          st_store(rec + R_ENT0 + q / 2, (uint64_t)ents[q] | (q + 1 < nent ? (uint64_t)ents[q + 1] << 32 : 0));
-        for (uint32_t o = 0; o < nout; o++) {
-          st_store(rec + R_OUT0 + 2 * o, outs[o][0]);
-          st_store(rec + R_OUT0 + 2 * o + 1, (outs[o][1] - ss) | ((outs[o][1] - outs[o][2]) << 20) |
-                                                 (outs[o][3] << 32));
+        if (lane >= 16 && lane < 16 + nout) {
+          const uint32_t o = lane - 16;
+          st_store(rec + R_OUT0 + 2 * o, L.outs[o][0]);
+          st_store(rec + R_OUT0 + 2 * o + 1, (L.outs[o][1] - ss) | ((L.outs[o][1] - L.outs[o][2]) << 20) |
+                                                 (L.outs[o][3] << 32));
         }
-        flag_publish(P.fA + seg, 1u);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(P.fA + seg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
 
+      stat_phase(P, ST_T_WALK, tstamp);
       // ---- 4. input state: exact, or speculated from the aggregates (wave)
       bool exact = false;
       cstate I = resolve_input(P, L, seg, lane, exact);
+      stat_phase(P, ST_T_INPUT, tstamp);
       const bool spec = !exact && !(I.st & S_NONE);
       uint64_t* rec = P.recs + seg * R_WORDS;
 
@@ -907,6 +998,7 @@ __global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
         }
       }
       if (stat_on(P)) stat_add(P, exact ? ST_EXACT_IN : spec ? ST_SPEC : ST_NOSPEC, 1);
+      stat_phase(P, ST_T_CHAIN, tstamp);
 
       // ---- 5b. own pair flag: assumed input == predecessor's published output
       bool ok = exact;
@@ -968,6 +1060,7 @@ __global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
         flag_publish(P.fV + seg, 1u);
       }
       if (stat_on(P) && ok && spec) stat_add(P, ST_VALID, 1);
+      stat_phase(P, ST_T_VALID, tstamp);
 
       // ---- 5c. frame count: aggregate + prefix (only ordinals need it) ------
       uint64_t n = rl64(lane == 0 ? c.o.cnt : 0, 0);
@@ -988,10 +1081,10 @@ __global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
         L.in = I;
         L.out = c.o;
         L.mode = c.mode;
-        L.ord_x = c.ordx;
-        L.out_x = c.outx;
-        L.npre = c.npre;
+        L.node_x = c.node;
+        L.rem_x = c.rem;
         L.nbase = nbase;
+        stat_phase(P, ST_T_COUNT, tstamp);
         if (stat_on(P)) {
           stat_add(P, c.mode == 2 ? ST_MODE2 : ST_MODE1, 1);
           stat_add(P, ST_NSURV, nsurv);
@@ -1028,9 +1121,13 @@ __global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
     }
     __syncthreads();
     if (mode == 1) {
-      const uint32_t ox = L.ord_x, oc = L.out_x, npre = L.npre;
-      if (tid < npre) {
-        const uint32_t i = L.s_ord_pre[tid];
+      // frame d of the path from node x is its d-th successor: binary lifting
+      const uint32_t x0 = L.node_x, rem = L.rem_x, base_n = L.nfl;
+      for (uint32_t dd = tid; dd < rem && base_n + dd < FCAP; dd += NT) {
+        uint32_t i = x0;
+#pragma unroll
+        for (uint32_t bb = 0; bb < LV; bb++)
+          if ((dd >> bb) & 1u) i = L.s_jmp[bb][i];
         const uint64_t p = ss + L.s_pos[i];
         const uint64_t ps = p + L.s_hlen[i];
         fent e;
@@ -1038,37 +1135,14 @@ __global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
         e.ps = (uint32_t)(ps - ss);
         e.end = L.s_nrel[i];
         e.kw = aligned_key(L.s_key[i], ps, 0);
-        L.flist[L.nfl + tid] = e;
+        L.flist[base_n + dd] = e;
         if (P.frames) {
           hdr_info hh = header_global(P.base, p, hi);
-          write_frame(P, fb + tid, p, hh, ps, 0);
+          write_frame(P, fb + dd, p, hh, ps, 0);
         }
       }
-      const uint32_t base_n = L.nfl + npre;
-      const uint64_t cbase = fb + npre;
-      uint32_t cnt = 0;
-      for (uint32_t i = tid; i < nsurv; i += NT) {
-        const uint16_t od = L.s_ord[i];
-        if (L.s_out[i] == oc && od != ORD_NONE && od >= ox) {
-          const uint64_t p = ss + L.s_pos[i];
-          const uint64_t ps = p + L.s_hlen[i];
-          fent e;
-          e.start = L.s_pos[i];
-          e.ps = (uint32_t)(ps - ss);
-          e.end = L.s_nrel[i];
-          e.kw = aligned_key(L.s_key[i], ps, 0);
-          L.flist[base_n + (od - ox)] = e;
-          if (P.frames) {
-            hdr_info hh = header_global(P.base, p, hi);
-            write_frame(P, cbase + (od - ox), p, hh, ps, 0);
-          }
-          cnt++;
-        }
-      }
-      cnt = wave_sum(cnt);
-      if (lane == 0) L.scan[wave] = cnt;
       __syncthreads();
-      if (tid == 0) L.nfl = base_n + L.scan[0] + L.scan[1] + L.scan[2] + L.scan[3];
+      if (tid == 0) L.nfl = base_n + rem;
     }
 
     for (;;) {
@@ -1121,6 +1195,7 @@ __global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
       __syncthreads();
     }
 
+    if (wid0(wave)) stat_phase(P, ST_T_XOR, tstamp);
     // ---- 6b. store changed chunks ------------------------------------------
     if (!parse_only) {
 #pragma unroll
@@ -1140,6 +1215,7 @@ __global__ void __launch_bounds__(NT, 2) k_stream_fused(st_params P) {
       }
     }
 
+    if (wid0(wave)) stat_phase(P, ST_T_STORE, tstamp);
     // ---- the last workgroup to finish: frame count + carry out -------------
     if (tid == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -1198,7 +1274,7 @@ __global__ void k_stream_empty(const xyws_carry* cin, xyws_carry* cout, uint64_t
   }
 }
 
-constexpr uint64_t HEAD_BYTES = 256;  // [0] ticket, [1] error, [64..128) carry snapshot, [128..256) stats
+constexpr uint64_t HEAD_BYTES = 512;  // [0] ticket, [1] error, [64..128) carry snapshot, [128..384) stats
 
 int occupancy_grid() {
   static int cached = 0;
@@ -1250,10 +1326,10 @@ int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
   return scratch_grow(s, (max_batch_bytes + 15 + SEG - 1) / SEG + 1);
 }
 
-int stream_scratch_stats(stream_scratch* s, uint64_t out[16]) {
+int stream_scratch_stats(stream_scratch* s, uint64_t out[32]) {
   if (!s->mem) return XYWS_ERR_INVALID;
   if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
-  return hipMemcpy(out, static_cast<uint8_t*>(s->mem) + 128, 128, hipMemcpyDeviceToHost) == hipSuccess
+  return hipMemcpy(out, static_cast<uint8_t*>(s->mem) + 128, 256, hipMemcpyDeviceToHost) == hipSuccess
              ? XYWS_OK : XYWS_ERR_HIP;
 }
 
@@ -1299,7 +1375,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   xyws_carry* snap = reinterpret_cast<xyws_carry*>(m + 64);
   if (hipMemsetAsync(P.head + 2, 0, 24, stream) != hipSuccess) return XYWS_ERR_HIP;  // done, total
   if (hipMemsetAsync(P.head, 0, 4, stream) != hipSuccess) return XYWS_ERR_HIP;
-  if ((opts & XYWS_OPT_STATS) && hipMemsetAsync(m + 128, 0, 128, stream) != hipSuccess) return XYWS_ERR_HIP;
+  if ((opts & XYWS_OPT_STATS) && hipMemsetAsync(m + 128, 0, 256, stream) != hipSuccess) return XYWS_ERR_HIP;
   if (cin) {
     if (hipMemcpyAsync(snap, cin, sizeof(xyws_carry), hipMemcpyDeviceToDevice, stream) != hipSuccess)
       return XYWS_ERR_HIP;
