@@ -81,3 +81,45 @@ def test_product_does_not_reference_oracle():
                 assert "oracle" not in src.replace("oracle/", "").lower() or f == "build.py", f
     out = subprocess.run(["ldd", L.lib_path()], capture_output=True, text=True).stdout
     assert "oracle" not in out and "xynet_ref" not in out
+
+
+SHIM_PROG = r"""
+#include <cstdio>
+#include "xyws/websocket.hpp"
+using namespace xyws;
+static_assert(detail::calc_frame_header_size(websocket_flags::WS_HAS_MASK, 65536) == 14);
+static_assert(detail::calc_frame_header_size(websocket_flags::WS_NONE, 125) == 2);
+static_assert(detail::calc_frame_size(websocket_flags::WS_HAS_MASK, 256) == 264);
+static_assert(websocket_flags_not_none(websocket_flags::WS_FIN | websocket_flags::WS_OP_TEXT));
+int main() {
+  try {
+    context ctx(0);
+    std::puts("device");
+    return 0;
+  } catch (const error& e) {
+    std::printf("error %d\n", e.code());
+    return 0;
+  }
+}
+"""
+
+
+def test_cpp_shim_compiles_links_and_fails_loudly(tmp_path):
+    """include/xyws/websocket.hpp (xynet names over the C-ABI) builds with g++
+    -std=c++20 against libxyws.so; without a GPU the context throws."""
+    src = tmp_path / "shim.cpp"
+    src.write_text(SHIM_PROG)
+    exe = tmp_path / "shim"
+    libdir = os.path.dirname(L.lib_path())
+    r = subprocess.run(["g++", "-std=c++20", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                        str(src), "-o", str(exe), "-L", libdir, "-lxyws", f"-Wl,-rpath,{libdir}"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    assert out.stdout.strip() == ("device" if has_gpu else "error -2")
