@@ -56,14 +56,41 @@ def load_golden():
         return json.load(f)["configs"]
 
 
-def build_batch(torch, T, cfg_name, rank, world):
-    """Generate this rank's batch in HBM; returns (buf, info)."""
+def shard_plan(cfg_name, rank, world):
+    """(seed, golden key, description) of this rank's batch. N > 1 on the
+    64 KiB config is config 5: rank g owns its own config-3-sized shard of
+    independent frames (seed 0x5EED0005 + g), so no rank needs another's data."""
     nframes, payload, b0, seed, gkey, desc = CONFIGS[cfg_name]
-    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     if cfg_name == "c3" and world > 1:
         seed, gkey = 0x5EED0005 + rank, f"c5_shard{rank}"
         desc = ("config 5 shard: 32768 x 64 KiB masked binary frames (H=14), one contiguous 2 GiB "
                 "batch per GPU, seed 0x5EED0005+rank")
+    return seed, gkey, desc
+
+
+def max_over_ranks(dist, torch, x, device):
+    """The slowest rank's value (the job's elapsed time); x itself at N = 1."""
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_ranks(dist, torch, ok, device):
+    """True only if every rank's flag is true (parity of every shard)."""
+    if dist is None:
+        return bool(ok)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def build_batch(torch, T, cfg_name, rank, world):
+    """Generate this rank's batch in HBM; returns (buf, info)."""
+    nframes, payload, b0, _, _, _ = CONFIGS[cfg_name]
+    seed, gkey, desc = shard_plan(cfg_name, rank, world)
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     if nframes is not None:
         size = nframes * (hdr_len(payload) + payload)
         buf = torch.empty(size, dtype=torch.uint8, device="cuda")
@@ -229,19 +256,14 @@ def main():
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(dist, torch, t1 - t0, "cuda")
     kernel_ms = sorted(a.elapsed_time(b) for a, b in evs)
     avg_ms = sum(kernel_ms) / len(kernel_ms)
 
     if args.stats and rank == 0:  # one extra counted decode pair (keeps the step parity)
-        names = ["exact_in", "spec", "no_spec", "valid", "slow", "recomputed", "no_anchor",
-                 "mode1", "mode2", "survivors", "spins", "-", "-", "-", "-", "-",
-                 "cyc_pass1", "cyc_walk", "cyc_input", "cyc_chain", "cyc_valid", "cyc_count",
-                 "cyc_xor", "cyc_store"]
+        names = ["exact_in", "spec", "fallback", "bad_pairs", "repaired", "mode1", "mode2",
+                 "survivors", "overflow", "segments", "-", "-", "-", "-", "-", "-",
+                 "cyc_index", "cyc_link", "cyc_input", "cyc_chain", "cyc_apply_list", "cyc_apply"]
         for _ in range(2):
             dec.opts |= 0x100
             dec.decode(buf, cap=0, count=False, carry=False)
@@ -249,7 +271,7 @@ def main():
             out = (C.c_uint64 * 32)()
             dec.ctx.L.xyws_debug_stats(dec.ctx.h, out)
         st = {k: v for k, v in zip(names, list(out)) if k != "-"}
-        nseg = max(1, st["mode1"] + st["mode2"])
+        nseg = max(1, st["segments"])
         for k in list(st):
             if k.startswith("cyc_"):
                 st[k.replace("cyc_", "us_per_seg_")] = round(st.pop(k) / nseg / 2100.0, 3)
@@ -267,11 +289,7 @@ def main():
     value = args.steps * total_payload / elapsed / GIB
     achieved = info["algo_bytes"] / (avg_ms * 1e-3) / 1e9
 
-    parities = [parity]
-    if dist:
-        flag = torch.tensor([1 if parity else 0], dtype=torch.int32, device="cuda")
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        parities = [bool(flag.item())]
+    parities = [all_ranks(dist, torch, parity, "cuda") if dist else parity]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

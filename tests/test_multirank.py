@@ -1,0 +1,59 @@
+"""N > 1 bench path on the CPU (gloo, world size 2): each rank plans its own
+shard of independent frames (config 5) with no data exchange, and only the
+timing max and the parity AND cross ranks — the same helpers bench.py runs
+over RCCL on the GPU node."""
+import json
+import os
+import socket
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+torch = pytest.importorskip("torch")
+dist = pytest.importorskip("torch.distributed")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as d
+    import bench
+    d.init_process_group("gloo", rank=rank, world_size=world)
+    seed, gkey, desc = bench.shard_plan("c3", rank, world)
+    elapsed = 1.0 + rank  # rank 1 is the slow one
+    t = bench.max_over_ranks(d, torch, elapsed, "cpu")
+    ok_all = bench.all_ranks(d, torch, True, "cpu")
+    ok_one_bad = bench.all_ranks(d, torch, rank == 0, "cpu")
+    d.barrier()
+    d.destroy_process_group()
+    with open(os.path.join(out_dir, f"r{rank}.json"), "w") as f:
+        json.dump(dict(seed=seed, gkey=gkey, desc=desc, t=t, ok_all=ok_all, ok_one_bad=ok_one_bad), f)
+
+
+def test_two_rank_gloo_shards_and_reductions(tmp_path):
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    res = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
+    cfgs = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))["configs"]
+    for r, x in enumerate(res):
+        assert x["seed"] == 0x5EED0005 + r
+        assert x["gkey"] == f"c5_shard{r}" and x["gkey"] in cfgs
+        assert x["t"] == 2.0                      # max over ranks
+        assert x["ok_all"] is True and x["ok_one_bad"] is False
+    assert res[0]["seed"] != res[1]["seed"]       # disjoint shards, no shared data
+
+
+def test_single_rank_plan_is_config3():
+    sys.path.insert(0, ROOT)
+    import bench
+    seed, gkey, _ = bench.shard_plan("c3", 0, 1)
+    assert (seed, gkey) == (0x5EED0003, "c3_bin_64k")
+    assert bench.max_over_ranks(None, torch, 3.5, "cpu") == 3.5
