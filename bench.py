@@ -263,7 +263,9 @@ def main():
     if args.stats and rank == 0:  # one extra counted decode pair (keeps the step parity)
         names = ["exact_in", "spec", "fallback", "bad_pairs", "repaired", "mode1", "mode2",
                  "survivors", "overflow", "segments", "-", "-", "-", "-", "-", "-",
-                 "cyc_index", "cyc_link", "cyc_input", "cyc_chain", "cyc_apply_list", "cyc_apply"]
+                 "cyc_index", "cyc_link", "cyc_input", "cyc_chain", "cyc_apply_list", "cyc_apply",
+                 "-", "-", "cyc_f_issue", "cyc_f_head", "cyc_f_poll", "cyc_f_recs", "cyc_f_stage0",
+                 "cyc_f_preapply", "cyc_f_accum"]
         for _ in range(2):
             dec.opts |= 0x100
             dec.decode(buf, cap=0, count=False, carry=False)

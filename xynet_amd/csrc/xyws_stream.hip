@@ -156,6 +156,7 @@ struct __attribute__((aligned(16))) st_lds {
   uint32_t bk[WIN][BKT];
   uint64_t seg_id, chase_X, fbase, nbase;
   cstate in, out;
+  uint64_t tstamp;            // wave 0's last s_memtime stamp (stats builds)
   uint32_t nfl, pass_done, nent_pub, nout_pub, mode, node_x, rem_x, flag, red, nowned;
   uint32_t owned[OWN_MAX];    // unmasked segments whose pair (k-1, k) is not yet checked
 };
@@ -178,12 +179,28 @@ struct st_params {
   uint32_t opts;
 };
 
+// The workgroup's LDS block and the launch parameters, reachable from every
+// stage function without passing pointers: a pointer parameter would be a
+// generic address, turning every LDS access into a flat instruction that also
+// waits on outstanding global loads. Parameters are read through the kernarg
+// segment (scalar loads).
+__shared__ st_lds g_L;
+typedef const __attribute__((address_space(4))) st_params kparams_t;
+XYWS_DEV st_params kparams() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(kparams_t*)(__builtin_amdgcn_kernarg_segment_ptr());
+#else
+  return st_params{};
+#endif
+}
+
 // ---------------------------------------------------------------- debug counters
 // With XYWS_OPT_STATS the kernel counts resolution events and per-phase
 // s_memtime cycles into the stats area (read back by xyws_debug_stats).
 enum { ST_EXACT_IN = 0, ST_SPEC, ST_FALLBACK, ST_BADPAIR, ST_REPAIR, ST_MODE1, ST_MODE2,
        ST_NSURV, ST_OVERFLOW, ST_SEGS,
        ST_T_INDEX = 16, ST_T_LINK, ST_T_INPUT, ST_T_CHAIN, ST_T_LIST, ST_T_APPLY,
+       ST_F_ISSUE = 24, ST_F_HEAD, ST_F_POLL, ST_F_RECS, ST_F_STAGE0, ST_F_PREAPPLY, ST_F_ACCUM,
        ST_NSTAT = 32 };
 
 // ---------------------------------------------------------------- hand-off
@@ -489,6 +506,7 @@ XYWS_DEV cstate resolve_input(const st_params& P, st_lds& L, uint64_t k, uint32_
   if (!__all(have)) atomicOr(P.head + 1, 64u);
   have = have && g >= 0;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  stat_phase(P, ST_F_POLL, L.tstamp);
   const uint64_t* r = rec_of(P, have ? (uint64_t)g : 0);
   const uint32_t meta = have ? (uint32_t)st_load(r + R_META) : 0u;
   uint64_t ent[NENT / 2], out[NOUT][2];
@@ -524,6 +542,7 @@ XYWS_DEV cstate resolve_input(const st_params& P, st_lds& L, uint64_t k, uint32_
     }
   }
   wave_sync();
+  stat_phase(P, ST_F_RECS, L.tstamp);
   // each segment: the first entry that some exit lands on -> its outcome
   const uint32_t nb = L.bk_n[lane] < BKT ? L.bk_n[lane] : BKT;
   uint32_t oc = 0xFFu;
@@ -670,7 +689,7 @@ XYWS_DEV __amdgpu_buffer_rsrc_t seg_rsrc(const st_params& P, uint64_t ss) {
 // ordinal fb when `emit`.
 XYWS_DEV void apply_frames(const st_params& P, st_lds& L, const sv_buf* S, uint64_t seg,
                            const cstate& sin, uint32_t mode, uint32_t node, uint32_t rem, uint64_t fb,
-                           bool emit, uint32_t tid) {
+                           bool emit, uint32_t tid, bool stamp = false) {
   const uint64_t ss = seg * SEG, se = ss + SEG, hi = P.hi;
   const bool parse_only = (P.opts & XYWS_OPT_PARSE_ONLY) != 0;
   emit = emit && P.frames;
@@ -761,6 +780,7 @@ XYWS_DEV void apply_frames(const st_params& P, st_lds& L, const sv_buf* S, uint6
     }
     __syncthreads();
   }
+  if (stamp && tid < 64) stat_phase(P, ST_F_ACCUM, L.tstamp);
   if (parse_only) return;
   // first/last chunk of the batch: only the caller's bytes (byte path)
   const uint64_t lim64 = hi - ss;
@@ -801,12 +821,13 @@ XYWS_DEV void apply_frames(const st_params& P, st_lds& L, const sv_buf* S, uint6
 }
 
 // ---------------------------------------------------------------- index stage
-__device__ __noinline__ void resolve_segment(const st_params& P, st_lds& L, const sv_buf& S, uint32_t lane,
-                                             uint64_t& tstamp);
+__device__ __noinline__ void resolve_segment(uint32_t buf, uint32_t lane);
 
-__device__ __noinline__ void index_segment(const st_params& P, st_lds& L, sv_buf& S, uint64_t seg,
-                                           const sv_buf* prev, uint32_t tid, uint32_t lane, uint32_t wave,
-                                           uint64_t& tstamp) {
+__device__ __noinline__ void index_segment(uint64_t seg, uint32_t buf, uint32_t prev, uint32_t tid,
+                                           uint32_t lane, uint32_t wave) {
+  const st_params P = kparams();
+  st_lds& L = g_L;
+  sv_buf& S = L.sv[buf];
   const bool want_unmasked = (P.opts & XYWS_OPT_UNMASKED_HINT) != 0;
   const uint64_t lo = P.lo, hi = P.hi;
   const uint64_t ss = seg * SEG;
@@ -820,13 +841,15 @@ __device__ __noinline__ void index_segment(const st_params& P, st_lds& L, sv_buf
   for (uint32_t k = 0; k < CHS; k++) d[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * NT * 16u, 0);
   u32x4 halo = {0u, 0u, 0u, 0u};
   if (tid == 0) halo = __builtin_amdgcn_raw_buffer_load_b128(rs, 0, SEG, 0);
+  if (tid == 0) { S.nsurv = 0; S.overflow = 0; S.seg = seg; }
+  if (wave == 0) stat_phase(P, ST_F_ISSUE, L.tstamp);
+  // the lagged segment's input and frames, while this segment's loads fly
+  if (prev < 3 && wave == 0) resolve_segment(prev, lane);
   if (tid < 2) {  // the segment's first 32 bytes, for headers straddling into it
     st_store(rec + R_HEAD + 2 * tid, (uint64_t)d[0].x | ((uint64_t)d[0].y << 32));
     st_store(rec + R_HEAD + 2 * tid + 1, (uint64_t)d[0].z | ((uint64_t)d[0].w << 32));
   }
-  if (tid == 0) { S.nsurv = 0; S.overflow = 0; S.seg = seg; }
-  // the lagged segment's input and frames, while this segment's loads fly
-  if (prev && wave == 0) resolve_segment(P, L, *prev, lane, tstamp);
+  if (wave == 0) stat_phase(P, ST_F_HEAD, L.tstamp);
 
   // ---- 1b. per sub-tile: LDS copy, prefilter, candidates -> survivors
 #pragma nounroll
@@ -843,6 +866,7 @@ __device__ __noinline__ void index_segment(const st_params& P, st_lds& L, sv_buf
       *reinterpret_cast<u32x4*>(&L.sub[SUB]) = v;
     }
     __syncthreads();
+    if (s == 0 && wave == 0) stat_phase(P, ST_F_STAGE0, L.tstamp);
     // prefilter: lane owns sub-tile positions [tid*32, tid*32+32)
     const uint32_t p0 = tid * PPL;
     uint32_t cand = 0;
@@ -923,7 +947,7 @@ __device__ __noinline__ void index_segment(const st_params& P, st_lds& L, sv_buf
     }
   }
   __syncthreads();
-  if (wave == 0) stat_phase(P, ST_T_INDEX, tstamp);
+  if (wave == 0) stat_phase(P, ST_T_INDEX, L.tstamp);
 
   // ---- 2. link survivors
   const uint32_t nsurv = S.overflow ? 0u : S.nsurv;
@@ -1068,7 +1092,7 @@ __device__ __noinline__ void index_segment(const st_params& P, st_lds& L, sv_buf
       stat_add(P, ST_NSURV, nsurv);
       if (S.overflow) stat_add(P, ST_OVERFLOW, 1);
     }
-    stat_phase(P, ST_T_LINK, tstamp);
+    stat_phase(P, ST_T_LINK, L.tstamp);
   }
 }
 
@@ -1076,12 +1100,15 @@ __device__ __noinline__ void index_segment(const st_params& P, st_lds& L, sv_buf
 // Steps 4-5 for the lagged segment (wave 0): input state, own frames, and the
 // (input, output, count) record stores — issued, not waited for. Runs inside
 // the next index stage, while that stage's segment loads are in flight.
-__device__ __noinline__ void resolve_segment(const st_params& P, st_lds& L, const sv_buf& S, uint32_t lane, uint64_t& tstamp) {
+__device__ __noinline__ void resolve_segment(uint32_t buf, uint32_t lane) {
+  const st_params P = kparams();
+  st_lds& L = g_L;
+  const sv_buf& S = L.sv[buf];
   const uint64_t seg = S.seg, ss = seg * SEG, se = ss + SEG;
   const uint32_t nsurv = S.overflow ? 0u : S.nsurv;
   uint32_t kind;
   const cstate I = resolve_input(P, L, seg, lane, kind);
-  stat_phase(P, ST_T_INPUT, tstamp);
+  stat_phase(P, ST_T_INPUT, L.tstamp);
   if (lane == 0) {
     const chain_res c = own_chain(P, S, nsurv, ss, se, I);
     if (c.mode != 2) {
@@ -1101,7 +1128,7 @@ __device__ __noinline__ void resolve_segment(const st_params& P, st_lds& L, cons
       stat_add(P, ST_SEGS, 1);
     }
   }
-  stat_phase(P, ST_T_CHAIN, tstamp);
+  stat_phase(P, ST_T_CHAIN, L.tstamp);
 }
 
 // Pair checks (whole workgroup) for the segments this workgroup unmasked:
@@ -1130,8 +1157,10 @@ XYWS_DEV void check_pairs(const st_params& P, st_lds& L, uint32_t tid) {
 // Step 6 (whole workgroup), after resolve_segment: descriptor ordinals (only
 // when descriptors are wanted), XOR application, then the (input, output)
 // flag and the frame count.
-__device__ __noinline__ void unmask_segment(const st_params& P, st_lds& L, const sv_buf& S, uint32_t tid,
-                                            uint32_t lane, uint32_t wave, uint64_t& tstamp) {
+__device__ __noinline__ void unmask_segment(uint32_t buf, uint32_t tid, uint32_t lane, uint32_t wave) {
+  const st_params P = kparams();
+  st_lds& L = g_L;
+  const sv_buf& S = L.sv[buf];
   const uint64_t seg = S.seg;
   uint64_t* rec = P.recs + seg * R_WORDS;
   if (tid == 0 && (P.frames || L.mode == 2)) {
@@ -1166,13 +1195,14 @@ __device__ __noinline__ void unmask_segment(const st_params& P, st_lds& L, const
     write_frame(P, 0, P.lo, hh, sin.cov_ps, (int32_t)P.cin->hdr_len);
   }
   if (tid == 0) flag_publish(P.fC + seg, 1u);  // record stores issued an index stage ago: no wait
-  apply_frames(P, L, &S, seg, sin, L.mode, L.node_x, L.rem_x, L.nbase + sin.cnt, true, tid);
+  if (wave == 0) stat_phase(P, ST_F_PREAPPLY, L.tstamp);
+  apply_frames(P, L, &S, seg, sin, L.mode, L.node_x, L.rem_x, L.nbase + sin.cnt, true, tid, true);
   if (tid == 0) {
     __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(P.head + 4), L.out.cnt, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     L.owned[L.nowned++] = (uint32_t)seg;
   }
-  if (wave == 0) stat_phase(P, ST_T_APPLY, tstamp);
+  if (wave == 0) stat_phase(P, ST_T_APPLY, L.tstamp);
   __syncthreads();
   if (L.nowned == OWN_MAX) check_pairs(P, L, tid);
 }
@@ -1211,7 +1241,9 @@ XYWS_DEV void emit_segment(const st_params& P, uint64_t j, const cstate& I, uint
 // The last workgroup to exit: repair mis-speculated segments, then the frame
 // count and the carry out. Whole workgroup; every other workgroup has exited
 // (its stores written back by its release fence).
-__device__ __noinline__ void finish(const st_params& P, st_lds& L, uint32_t tid, uint64_t& tstamp) {
+__device__ __noinline__ void finish(uint32_t tid) {
+  const st_params P = kparams();
+  st_lds& L = g_L;
   const uint64_t nseg = P.nseg;
   int64_t delta = 0;
   cstate E = load_state(rec_of(P, nseg - 1) + R_CO);
@@ -1295,7 +1327,6 @@ __device__ __noinline__ void finish(const st_params& P, st_lds& L, uint32_t tid,
       *P.cout = c;
     }
   }
-  (void)tstamp;
 }
 
 // ---------------------------------------------------------------- kernel
@@ -1304,9 +1335,9 @@ __device__ __noinline__ void finish(const st_params& P, st_lds& L, uint32_t tid,
 // loop and held in VGPRs for the whole kernel (125 spilled VGPRs); as calls,
 // each stage allocates its own registers and nothing spills.
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) k_stream_fused(st_params P) {  // 2 workgroups = 16 waves per CU (<= 128 VGPRs)
-  __shared__ st_lds L;
+  st_lds& L = g_L;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  uint64_t tstamp = stat_on(P) ? __builtin_amdgcn_s_memtime() : 0;
+  if (tid == 0) L.tstamp = stat_on(P) ? __builtin_amdgcn_s_memtime() : 0;
   // three survivor buffers: the segment being indexed and the two indexed
   // before it; the older one is resolved inside the index stage and unmasked
   // after it (lag 2), so everything it waits for was published a stage ago
@@ -1317,15 +1348,15 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4)))
     __syncthreads();
     const uint64_t t = L.seg_id;
     const bool more = t < P.nseg;
-    const sv_buf* old = (npend == 2 || (!more && npend > 0)) ? &L.sv[(cur + 3 - npend) % 3] : nullptr;
+    const uint32_t old = (npend == 2 || (!more && npend > 0)) ? (cur + 3 - npend) % 3 : 3u;  // 3: none
     if (more) {
-      index_segment(P, L, L.sv[cur], t, old, tid, lane, wave, tstamp);
-    } else if (old && wave == 0) {
-      resolve_segment(P, L, *old, lane, tstamp);
+      index_segment(t, cur, old, tid, lane, wave);
+    } else if (old < 3 && wave == 0) {
+      resolve_segment(old, lane);
     }
-    if (old) {
+    if (old < 3) {
       __syncthreads();
-      unmask_segment(P, L, *old, tid, lane, wave, tstamp);
+      unmask_segment(old, tid, lane, wave);
       npend--;
     }
     if (more) {
@@ -1347,7 +1378,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4)))
   __syncthreads();
   if (L.flag) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    finish(P, L, tid, tstamp);
+    finish(tid);
   }
 }
 
