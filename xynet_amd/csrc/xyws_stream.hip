@@ -68,17 +68,17 @@
 namespace {
 
 constexpr uint32_t SEG = 65536;            // segment bytes
-constexpr uint32_t SUB = 16384;            // sub-tile bytes staged in LDS
-constexpr uint32_t NSUB = SEG / SUB;       // 4
-constexpr uint32_t NT = 512;               // threads per workgroup (8 waves)
+constexpr uint32_t SUB = 8192;             // sub-tile bytes staged in LDS
+constexpr uint32_t NSUB = SEG / SUB;       // 8
+constexpr uint32_t NT = 256;               // threads per workgroup (4 waves)
 constexpr uint32_t NW = NT / 64;           // waves per workgroup
-constexpr uint32_t CHS = SEG / (16 * NT);  // 8 chunks of 16 B per lane
+constexpr uint32_t CHS = SEG / (16 * NT);  // 16 chunks of 16 B per lane
 constexpr uint32_t CHSUB = SUB / (16 * NT);  // 2 per sub-tile
 constexpr uint32_t PPL = SUB / NT;         // prefilter positions per lane (32)
 constexpr uint32_t HALO = 16;
 constexpr uint32_t SMAX = 512;             // survivors tracked per segment
 constexpr uint32_t LV = 9;                 // jump-table levels: 2^LV >= SMAX
-constexpr uint32_t NPT = SMAX / NT;        // survivor nodes per thread (1)
+constexpr uint32_t NPT = SMAX / NT;        // survivor nodes per thread (2)
 constexpr uint32_t FCAP = SUB / 16;        // frame-list entries per pass (overlays the sub-tile)
 constexpr uint32_t NENT = 16;              // aggregate entry nodes (2 per record word)
 constexpr uint32_t NOUT = 8;               // aggregate outcomes (2 record words each)
@@ -86,7 +86,6 @@ constexpr uint32_t SPIN = 1u << 24;        // bounded spins (~1 s)
 constexpr uint32_t WIN = 64;               // segments seen by one speculation (one per lane)
 constexpr uint32_t BKT = 8;                // exits kept per target segment during speculation
 constexpr uint32_t OOB = 0x80000000u;      // buffer offset past every range: load 0, store dropped
-constexpr uint32_t OWN_MAX = 256;          // segments a workgroup remembers for its pair checks
 
 constexpr uint16_t N_EXIT = 0xFFFF, N_DEAD = 0xFFFE;
 constexpr uint8_t O_DEAD = 0xFE, O_UNREC = 0xFD;  // node outcome marks
@@ -149,7 +148,7 @@ struct __attribute__((aligned(16))) st_lds {
   uint32_t bits[SUB / 32];    // candidate bitmap of the current sub-tile
   uint16_t nxt[SMAX];         // index: successor survivor / N_EXIT / N_DEAD
   uint16_t last[SMAX];        // index: chain end (T_DEAD: dead end)
-  sv_buf sv[3];               // indexed, awaiting unmask (lag 2), being indexed
+  sv_buf sv;
   uint32_t scan[8];
   uint32_t ents[NENT];
   uint32_t bk_n[WIN];         // speculation: exits landing in each window segment
@@ -157,8 +156,7 @@ struct __attribute__((aligned(16))) st_lds {
   uint64_t seg_id, chase_X, fbase, nbase;
   cstate in, out;
   uint64_t tstamp;            // wave 0's last s_memtime stamp (stats builds)
-  uint32_t nfl, pass_done, nent_pub, nout_pub, mode, node_x, rem_x, flag, red, nowned;
-  uint32_t owned[OWN_MAX];    // unmasked segments whose pair (k-1, k) is not yet checked
+  uint32_t nfl, pass_done, nent_pub, nout_pub, mode, node_x, rem_x, red;
 };
 
 struct st_params {
@@ -731,11 +729,18 @@ XYWS_DEV void apply_frames(const st_params& P, st_lds& L, const sv_buf* S, uint6
     __syncthreads();
     if (tid == 0) L.nfl = base_n + rem;
   }
-  u32x4 x[CHS];
-#pragma unroll
-  for (uint32_t k = 0; k < CHS; k++) x[k] = u32x4{0u, 0u, 0u, 0u};
+  // Passes of at most FCAP entries. Pass p applies the chunks in [lo_c, hi_c):
+  // hi_c = the chunk-aligned start of its last frame (SEG for the final pass);
+  // the frames reaching past hi_c carry into the next pass. Every chunk is
+  // loaded, XORed and stored once, its loads issued before its XOR words are
+  // built.
+  const __amdgpu_buffer_rsrc_t rs = seg_rsrc(P, ss);
+  const uint32_t voff = tid * 16u;
+  const uint64_t lim64 = hi - ss;
+  const uint32_t lim = lim64 < SEG ? (uint32_t)lim64 : SEG;  // bytes of this segment in the batch
+  uint32_t lo_c = 0;
   for (;;) {
-    if (mode == 2 && tid == 0) {  // exact chase, FCAP entries per pass
+    if (mode == 2 && tid == 0) {  // exact chase, up to FCAP entries per pass
       uint64_t X = L.chase_X, ord = L.fbase;
       uint32_t n = L.nfl;
       const uint64_t stop = se < hi ? se : hi;
@@ -760,74 +765,63 @@ XYWS_DEV void apply_frames(const st_params& P, st_lds& L, const sv_buf* S, uint6
     }
     __syncthreads();
     const uint32_t nfl = L.nfl;
+    const uint32_t done = L.pass_done;
+    const uint32_t hi_c = (done || !nfl) ? SEG : (L.flist[nfl - 1].start & ~15u);
     if (!parse_only && nfl) {
-      uint32_t g = 0;
+      u32x4 d[CHS];
+#pragma unroll
+      for (uint32_t k = 0; k < CHS; k++) {
+        const uint32_t a = (k * NT + tid) * 16u;
+        d[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (a >= lo_c && a < hi_c) ? voff : OOB, k * NT * 16u, 0);
+      }
+      uint32_t g = 0, edge = 0;
 #pragma unroll
       for (uint32_t k = 0; k < CHS; k++) {
         const uint32_t a = (k * NT + tid) * 16u;  // increases with k: g only moves forward
         while (g + 1 < nfl && L.flist[g + 1].start <= a) g++;
-        x[k] |= chunk_xor(L, nfl, g, a);
+        const u32x4 x = chunk_xor(L, nfl, g, a);
+        const bool nz = (x.x | x.y | x.z | x.w) != 0u;
+        const bool inr = a >= lo_c && a < hi_c;
+        const bool inb = a + 16 <= lim && !(ss == 0 && a < P.lo);
+        __builtin_amdgcn_raw_buffer_store_b128(d[k] ^ x, rs, (inr && nz && inb) ? voff : OOB, k * NT * 16u, 0);
+        if (inr && nz && !inb) edge |= 1u << k;
+      }
+      // first/last chunk of the batch: only the caller's bytes (rare, not unrolled)
+#pragma nounroll
+      while (edge) {
+        const uint32_t k = __builtin_ctz(edge);
+        edge &= edge - 1;
+        const uint32_t a = (k * NT + tid) * 16u;
+        uint32_t ge = 0;
+        while (ge + 1 < nfl && L.flist[ge + 1].start <= a) ge++;
+        const u32x4 x = chunk_xor(L, nfl, ge, a);
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma nounroll
+        for (uint32_t t = 0; t < 16; t++) {
+          const uint64_t q = ss + a + t;
+          const uint8_t kb = (uint8_t)(w[t >> 2] >> (8u * (t & 3u)));
+          if (kb && q >= P.lo && q < hi) P.base[q] ^= kb;
+        }
       }
     }
-    const uint32_t done = L.pass_done;
+    if (stamp && tid < 64 && done) stat_phase(P, ST_F_ACCUM, L.tstamp);
     __syncthreads();
     if (done) break;
-    if (tid == 0) {  // next pass: the last frame becomes the covering entry
-      fent e = L.flist[L.nfl - 1];
-      e.start = 0;
-      L.flist[0] = e;
-      L.nfl = 1;
+    if (tid == 0) {  // carry the frames reaching past hi_c into the next pass
+      uint32_t c = nfl;
+      while (c > 0 && L.flist[c - 1].end > hi_c) c--;
+      for (uint32_t i = c; i < nfl; i++) L.flist[i - c] = L.flist[i];
+      L.nfl = nfl - c;
     }
+    lo_c = hi_c;
     __syncthreads();
-  }
-  if (stamp && tid < 64) stat_phase(P, ST_F_ACCUM, L.tstamp);
-  if (parse_only) return;
-  // first/last chunk of the batch: only the caller's bytes (byte path)
-  const uint64_t lim64 = hi - ss;
-  const uint32_t lim = lim64 < SEG ? (uint32_t)lim64 : SEG;
-#pragma unroll
-  for (uint32_t k = 0; k < CHS; k++) {
-    const uint32_t c16 = (k * NT + tid) * 16u;
-    const bool inb = c16 + 16 <= lim && !(ss == 0 && c16 < P.lo);
-    if (!inb && (x[k].x | x[k].y | x[k].z | x[k].w)) {
-      const uint32_t w[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
-      for (uint32_t t = 0; t < 16; t++) {
-        const uint64_t q = ss + c16 + t;
-        const uint8_t kb = (uint8_t)(w[t >> 2] >> (8u * (t & 3u)));
-        if (kb && q >= P.lo && q < hi) P.base[q] ^= kb;
-      }
-      x[k] = u32x4{0u, 0u, 0u, 0u};
-    }
-  }
-  // load, XOR, store the changed chunks (unchanged ones get an out-of-range
-  // offset: no load, no store), eight in flight at a time
-  const __amdgpu_buffer_rsrc_t rs = seg_rsrc(P, ss);
-  const uint32_t voff = tid * 16u;
-#pragma unroll
-  for (uint32_t h = 0; h < CHS; h += 8) {
-    u32x4 d[8];
-#pragma unroll
-    for (uint32_t k = 0; k < 8; k++) {
-      const bool nz = (x[h + k].x | x[h + k].y | x[h + k].z | x[h + k].w) != 0u;
-      d[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, nz ? voff : OOB, (h + k) * NT * 16u, 0);
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < 8; k++) {
-      const bool nz = (x[h + k].x | x[h + k].y | x[h + k].z | x[h + k].w) != 0u;
-      __builtin_amdgcn_raw_buffer_store_b128(d[k] ^ x[h + k], rs, nz ? voff : OOB, (h + k) * NT * 16u, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 // ---------------------------------------------------------------- index stage
-__device__ __noinline__ void resolve_segment(uint32_t buf, uint32_t lane);
-
-__device__ __noinline__ void index_segment(uint64_t seg, uint32_t buf, uint32_t prev, uint32_t tid,
-                                           uint32_t lane, uint32_t wave) {
-  const st_params P = kparams();
-  st_lds& L = g_L;
-  sv_buf& S = L.sv[buf];
+XYWS_DEV void index_segment(const st_params& P, st_lds& L, uint64_t seg, uint32_t tid, uint32_t lane,
+                            uint32_t wave) {
+  sv_buf& S = L.sv;
   const bool want_unmasked = (P.opts & XYWS_OPT_UNMASKED_HINT) != 0;
   const uint64_t lo = P.lo, hi = P.hi;
   const uint64_t ss = seg * SEG;
@@ -843,8 +837,6 @@ __device__ __noinline__ void index_segment(uint64_t seg, uint32_t buf, uint32_t 
   if (tid == 0) halo = __builtin_amdgcn_raw_buffer_load_b128(rs, 0, SEG, 0);
   if (tid == 0) { S.nsurv = 0; S.overflow = 0; S.seg = seg; }
   if (wave == 0) stat_phase(P, ST_F_ISSUE, L.tstamp);
-  // the lagged segment's input and frames, while this segment's loads fly
-  if (prev < 3 && wave == 0) resolve_segment(prev, lane);
   if (tid < 2) {  // the segment's first 32 bytes, for headers straddling into it
     st_store(rec + R_HEAD + 2 * tid, (uint64_t)d[0].x | ((uint64_t)d[0].y << 32));
     st_store(rec + R_HEAD + 2 * tid + 1, (uint64_t)d[0].z | ((uint64_t)d[0].w << 32));
@@ -856,15 +848,13 @@ __device__ __noinline__ void index_segment(uint64_t seg, uint32_t buf, uint32_t 
   for (uint32_t s = 0; s < NSUB; s++) {
     const uint64_t ts = ss + (uint64_t)s * SUB, te = ts + SUB;
     __syncthreads();  // previous sub-tile (or the previous unmask stage's list) consumed
+    // sub-tile s is always d[0 .. CHSUB): the chunk registers shift down by
+    // CHSUB after each sub-tile (register moves, no dynamic indexing)
 #pragma unroll
-    for (uint32_t k = 0; k < CHSUB; k++) {
-      const u32x4 v = s == 0 ? d[k] : s == 1 ? d[CHSUB + k] : s == 2 ? d[2 * CHSUB + k] : d[3 * CHSUB + k];
-      *reinterpret_cast<u32x4*>(&L.sub[(k * NT + tid) * 16u]) = v;
-    }
-    if (tid == 0) {
-      const u32x4 v = s == 0 ? d[CHSUB] : s == 1 ? d[2 * CHSUB] : s == 2 ? d[3 * CHSUB] : halo;
-      *reinterpret_cast<u32x4*>(&L.sub[SUB]) = v;
-    }
+    for (uint32_t k = 0; k < CHSUB; k++) *reinterpret_cast<u32x4*>(&L.sub[(k * NT + tid) * 16u]) = d[k];
+    if (tid == 0) *reinterpret_cast<u32x4*>(&L.sub[SUB]) = s + 1 < NSUB ? d[CHSUB] : halo;
+#pragma unroll
+    for (uint32_t k = 0; k + CHSUB < CHS; k++) d[k] = d[k + CHSUB];
     __syncthreads();
     if (s == 0 && wave == 0) stat_phase(P, ST_F_STAGE0, L.tstamp);
     // prefilter: lane owns sub-tile positions [tid*32, tid*32+32)
@@ -1100,10 +1090,8 @@ __device__ __noinline__ void index_segment(uint64_t seg, uint32_t buf, uint32_t 
 // Steps 4-5 for the lagged segment (wave 0): input state, own frames, and the
 // (input, output, count) record stores — issued, not waited for. Runs inside
 // the next index stage, while that stage's segment loads are in flight.
-__device__ __noinline__ void resolve_segment(uint32_t buf, uint32_t lane) {
-  const st_params P = kparams();
-  st_lds& L = g_L;
-  const sv_buf& S = L.sv[buf];
+XYWS_DEV void resolve_segment(const st_params& P, st_lds& L, uint32_t lane) {
+  const sv_buf& S = L.sv;
   const uint64_t seg = S.seg, ss = seg * SEG, se = ss + SEG;
   const uint32_t nsurv = S.overflow ? 0u : S.nsurv;
   uint32_t kind;
@@ -1131,36 +1119,11 @@ __device__ __noinline__ void resolve_segment(uint32_t buf, uint32_t lane) {
   stat_phase(P, ST_T_CHAIN, L.tstamp);
 }
 
-// Pair checks (whole workgroup) for the segments this workgroup unmasked:
-// k's assumed input against k-1's published output.
-XYWS_DEV void check_pairs(const st_params& P, st_lds& L, uint32_t tid) {
-  __syncthreads();
-  const uint32_t n = L.nowned;
-  for (uint32_t i = tid; i < n; i += NT) {
-    const uint64_t k = L.owned[i];
-    if (k == 0) continue;  // segment 0's input is exact
-    spin_for(P.fC + k - 1, 1u, P.head + 1, 128u);
-    const cstate a = load_state(rec_of(P, k) + R_CI);
-    const cstate b = load_state(rec_of(P, k - 1) + R_CO);
-    const bool ok = same_state(a, b);
-    __hip_atomic_store(P.fP + k, ok ? 1u : 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!ok) {
-      atomicOr(P.head + 3, 1u);
-      if (stat_on(P)) atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + ST_BADPAIR, 1ull);
-    }
-  }
-  __syncthreads();
-  if (tid == 0) L.nowned = 0;
-  __syncthreads();
-}
-
 // Step 6 (whole workgroup), after resolve_segment: descriptor ordinals (only
 // when descriptors are wanted), XOR application, then the (input, output)
 // flag and the frame count.
-__device__ __noinline__ void unmask_segment(uint32_t buf, uint32_t tid, uint32_t lane, uint32_t wave) {
-  const st_params P = kparams();
-  st_lds& L = g_L;
-  const sv_buf& S = L.sv[buf];
+XYWS_DEV void unmask_segment(const st_params& P, st_lds& L, uint32_t tid, uint32_t lane, uint32_t wave) {
+  const sv_buf& S = L.sv;
   const uint64_t seg = S.seg;
   uint64_t* rec = P.recs + seg * R_WORDS;
   if (tid == 0 && (P.frames || L.mode == 2)) {
@@ -1194,17 +1157,14 @@ __device__ __noinline__ void unmask_segment(uint32_t buf, uint32_t tid, uint32_t
     hdr_info hh = header_carried(P.base, P.lo, P.hi, P.cin);
     write_frame(P, 0, P.lo, hh, sin.cov_ps, (int32_t)P.cin->hdr_len);
   }
-  if (tid == 0) flag_publish(P.fC + seg, 1u);  // record stores issued an index stage ago: no wait
   if (wave == 0) stat_phase(P, ST_F_PREAPPLY, L.tstamp);
   apply_frames(P, L, &S, seg, sin, L.mode, L.node_x, L.rem_x, L.nbase + sin.cnt, true, tid, true);
+  if (wave == 0) stat_phase(P, ST_T_APPLY, L.tstamp);
   if (tid == 0) {
     __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(P.head + 4), L.out.cnt, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-    L.owned[L.nowned++] = (uint32_t)seg;
+    flag_publish(P.fC + seg, 1u);  // (input, output) for fallback inputs of later segments
   }
-  if (wave == 0) stat_phase(P, ST_T_APPLY, L.tstamp);
-  __syncthreads();
-  if (L.nowned == OWN_MAX) check_pairs(P, L, tid);
 }
 
 // ---------------------------------------------------------------- finish
@@ -1241,13 +1201,11 @@ XYWS_DEV void emit_segment(const st_params& P, uint64_t j, const cstate& I, uint
 // The last workgroup to exit: repair mis-speculated segments, then the frame
 // count and the carry out. Whole workgroup; every other workgroup has exited
 // (its stores written back by its release fence).
-__device__ __noinline__ void finish(uint32_t tid) {
-  const st_params P = kparams();
-  st_lds& L = g_L;
+XYWS_DEV void finish(const st_params& P, st_lds& L, uint32_t tid) {
   const uint64_t nseg = P.nseg;
   int64_t delta = 0;
   cstate E = load_state(rec_of(P, nseg - 1) + R_CO);
-  if (flag_load(P.head + 3)) {
+  if (flag_load(P.head + 3)) {  // some pair failed: repair in order from the first
     uint64_t k = next_bad(P, L, 1, tid);
     if (k < nseg) E = load_state(rec_of(P, k - 1) + R_CO);
     while (k < nseg) {
@@ -1329,58 +1287,41 @@ __device__ __noinline__ void finish(uint32_t tid) {
   }
 }
 
-// ---------------------------------------------------------------- kernel
-// The stages are out-of-line calls on purpose: inlined into the persistent
-// loop, every thread-id-derived address of every stage is hoisted out of the
-// loop and held in VGPRs for the whole kernel (125 spilled VGPRs); as calls,
-// each stage allocates its own registers and nothing spills.
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) k_stream_fused(st_params P) {  // 2 workgroups = 16 waves per CU (<= 128 VGPRs)
+// ---------------------------------------------------------------- kernels
+// One workgroup per segment, in ticket order (so every segment a workgroup
+// waits for belongs to a workgroup that started earlier). Straight-line: index,
+// resolve (wave 0), unmask. 4 workgroups = 16 waves per CU (<= 128 VGPRs,
+// <= 40 KiB LDS each): while some wait on memory or on predecessors, others run.
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) k_stream_fused(st_params P) {
   st_lds& L = g_L;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  if (tid == 0) L.tstamp = stat_on(P) ? __builtin_amdgcn_s_memtime() : 0;
-  // three survivor buffers: the segment being indexed and the two indexed
-  // before it; the older one is resolved inside the index stage and unmasked
-  // after it (lag 2), so everything it waits for was published a stage ago
-  uint32_t cur = 0, npend = 0;
-  if (tid == 0) L.nowned = 0;
-  for (;;) {
-    if (tid == 0) L.seg_id = atomicAdd(P.head, 1u);
-    __syncthreads();
-    const uint64_t t = L.seg_id;
-    const bool more = t < P.nseg;
-    const uint32_t old = (npend == 2 || (!more && npend > 0)) ? (cur + 3 - npend) % 3 : 3u;  // 3: none
-    if (more) {
-      index_segment(t, cur, old, tid, lane, wave);
-    } else if (old < 3 && wave == 0) {
-      resolve_segment(old, lane);
-    }
-    if (old < 3) {
-      __syncthreads();
-      unmask_segment(old, tid, lane, wave);
-      npend--;
-    }
-    if (more) {
-      npend++;
-      cur = cur == 2 ? 0 : cur + 1;
-    } else if (npend == 0) {
-      break;
-    }
-  }
-  // exit: check the remaining pairs, write back every byte this workgroup
-  // stored, then count out; the last one out finishes the batch
-  check_pairs(P, L, tid);
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const uint32_t done = atomicAdd(P.head + 2, 1u);
-    L.flag = done == gridDim.x - 1;
-    if (L.flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    L.seg_id = atomicAdd(P.head, 1u);
+    L.tstamp = stat_on(P) ? __builtin_amdgcn_s_memtime() : 0;
   }
   __syncthreads();
-  if (L.flag) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    finish(tid);
+  const uint64_t seg = L.seg_id;
+  index_segment(P, L, seg, tid, lane, wave);
+  if (wave == 0) resolve_segment(P, L, lane);
+  __syncthreads();
+  unmask_segment(P, L, tid, lane, wave);
+}
+
+// Pair checks after the decode: segment k's assumed input against segment
+// k-1's output (one thread per pair; the kernel boundary orders the records).
+__global__ void __launch_bounds__(256) k_stream_pairs(st_params P) {
+  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x + 1;
+  if (k >= P.nseg) return;
+  const bool ok = same_state(load_state(rec_of(P, k) + R_CI), load_state(rec_of(P, k - 1) + R_CO));
+  P.fP[k] = ok ? 1u : 2u;
+  if (!ok) {
+    atomicOr(P.head + 3, 1u);
+    if (stat_on(P)) atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + ST_BADPAIR, 1ull);
   }
 }
+
+// Repairs (if any pair failed), the frame count and the carry out.
+__global__ void __launch_bounds__(NT) k_stream_finish(st_params P) { finish(P, g_L, threadIdx.x); }
 
 // Empty batch: the state passes through unchanged.
 __global__ void k_stream_empty(const xyws_carry* cin, xyws_carry* cout, uint64_t* nframes) {
@@ -1395,19 +1336,6 @@ __global__ void k_stream_empty(const xyws_carry* cin, xyws_carry* cout, uint64_t
 }
 
 constexpr uint64_t HEAD_BYTES = 512;  // [0] ticket .. [5]; [64..128) carry snapshot; [128..384) stats
-
-int occupancy_grid() {
-  static int cached = 0;
-  if (cached) return cached;
-  int dev = 0, cus = 256, per = 2;
-  (void)hipGetDevice(&dev);
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_stream_fused, NT, 0) != hipSuccess || per < 1)
-    per = 2;
-  cached = cus * per;
-  return cached;
-}
 
 }  // namespace
 
@@ -1502,8 +1430,9 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   }
   P.cin = snap;
   if (hipMemsetAsync(fl, 0, (4 * nseg * 4 + 15) & ~15ull, stream) != hipSuccess) return XYWS_ERR_HIP;
-  int grid = occupancy_grid();
-  if ((uint64_t)grid > nseg) grid = (int)nseg;
-  hipLaunchKernelGGL(k_stream_fused, dim3(grid), dim3(NT), 0, stream, P);
+  hipLaunchKernelGGL(k_stream_fused, dim3((uint32_t)nseg), dim3(NT), 0, stream, P);
+  if (nseg > 1)
+    hipLaunchKernelGGL(k_stream_pairs, dim3((uint32_t)((nseg - 1 + 255) / 256)), dim3(256), 0, stream, P);
+  hipLaunchKernelGGL(k_stream_finish, dim3(1), dim3(NT), 0, stream, P);
   return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
