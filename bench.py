@@ -215,6 +215,7 @@ def main():
     ap.add_argument("--host-path", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--stats", action="store_true", help="print fused-decoder resolution counters")
+    ap.add_argument("--xopts", type=lambda x: int(x, 0), default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     import torch
@@ -232,6 +233,7 @@ def main():
     buf, info = build_batch(torch, T, args.config, rank, world)
     golden = load_golden().get(info["golden"])
     dec = ws.frame_decoder(serial=(args.mode == "serial"))
+    dec.opts |= args.xopts
     dec.ctx.reserve(buf.numel(), 0)
     stream = torch.cuda.current_stream()
 
@@ -261,11 +263,9 @@ def main():
     avg_ms = sum(kernel_ms) / len(kernel_ms)
 
     if args.stats and rank == 0:  # one extra counted decode pair (keeps the step parity)
-        names = ["exact_in", "spec", "fallback", "bad_pairs", "repaired", "mode1", "mode2",
-                 "survivors", "overflow", "segments", "-", "-", "-", "-", "-", "-",
-                 "cyc_index", "cyc_link", "cyc_input", "cyc_chain", "cyc_apply_list", "cyc_apply",
-                 "-", "-", "cyc_f_issue", "cyc_f_head", "cyc_f_poll", "cyc_f_recs", "cyc_f_stage0",
-                 "cyc_f_preapply", "cyc_f_accum"]
+        names = ["runs", "runs_without_entry", "bad_boundaries", "repairs", "cuts", "spins", "segments",
+                 "frames", "-", "-", "-", "-", "-", "-", "-", "-", "cyc_prologue", "cyc_main", "cyc_wait",
+                 "cyc_fill", "cyc_chase_sync", "cyc_xor", "cyc_tail", "cyc_prefetch_issue", "cyc_chase_pass"]
         for _ in range(2):
             dec.opts |= 0x100
             dec.decode(buf, cap=0, count=False, carry=False)
@@ -273,10 +273,10 @@ def main():
             out = (C.c_uint64 * 32)()
             dec.ctx.L.xyws_debug_stats(dec.ctx.h, out)
         st = {k: v for k, v in zip(names, list(out)) if k != "-"}
-        nseg = max(1, st["segments"])
+        nrun = max(1, st["runs"] + 1)
         for k in list(st):
             if k.startswith("cyc_"):
-                st[k.replace("cyc_", "us_per_seg_")] = round(st.pop(k) / nseg / 2100.0, 3)
+                st[k.replace("cyc_", "us_per_run_")] = round(st.pop(k) / nrun / 2100.0, 3)
         print(json.dumps({"stats": st}), flush=True)
 
     # parity after the timed region: total decodes = warmup + steps

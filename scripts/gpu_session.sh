@@ -19,7 +19,7 @@ run() {  # name seconds cmd...
 }
 for step in "$@"; do
   case $step in
-    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -x -q ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     tests_all) run pytest_gpu 1200 python -m pytest tests -m gpu -q ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-MODES = {"fused": False, "serial": True}
+MODES = {"fused": {}, "serial": {"serial": True}, "runs1k": {"small_segments": True}}
 
 
 @pytest.fixture(scope="module")
@@ -91,7 +91,7 @@ def test_stream_edge_cases(ws, oracle, name, mode):
     src = streams.case_bytes(name)
     for off in (0, 5):
         view, whole = dev_bytes(src, off)
-        dec = ws.frame_decoder(serial=MODES[mode])
+        dec = ws.frame_decoder(**MODES[mode])
         cap = g["nframes"] + 4
         r = dec.decode(view, cap=cap)
         assert r.nframes == g["nframes"]
@@ -120,7 +120,7 @@ def test_stream_split_with_carry(ws, name, mode):
         k = s["k"]
         a, wa = dev_bytes(src[:k])
         b, wb = dev_bytes(src[k:])
-        dec = ws.frame_decoder(serial=MODES[mode])
+        dec = ws.frame_decoder(**MODES[mode])
         ra = dec.decode(a, cap=g["nframes"] + 2)
         assert ra.nframes == s["n1"]
         assert carry_list(dec.carry()) == s["carry_mid"], (name, k)
@@ -134,15 +134,16 @@ def test_stream_split_with_carry(ws, name, mode):
         assert [[x[0] + k, x[1] + k] + x[2:] for x in fb] == g["frames"][s["n1"]:]
 
 
-def test_fuzz_random_streams_vs_oracle(ws, oracle):
-    """Random frame soups + random cut points, GPU (fused) vs oracle."""
+@pytest.mark.parametrize("mode", ["fused", "runs1k"])
+def test_fuzz_random_streams_vs_oracle(ws, oracle, mode):
+    """Random frame soups + random cut points, GPU vs oracle."""
     rng = streams.SplitMix(0xF022)
     for it in range(40):
         n = 1 + rng.below(300)
         src = streams.case_bytes(f"random_frames_{n}") if it % 2 else streams.SplitMix(it).bytes(
             rng.below(200000))
         cuts = sorted(set([0, len(src)] + [rng.below(len(src) + 1) for _ in range(rng.below(4))]))
-        dec = ws.frame_decoder()
+        dec = ws.frame_decoder(**MODES[mode])
         carry = None
         for a, b in zip(cuts[:-1], cuts[1:]):
             piece = src[a:b]
@@ -234,12 +235,14 @@ def dev_digest(buf):
     return int(out[0].item()) & ((1 << 64) - 1)
 
 
-@pytest.mark.parametrize("name", ["t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m", "c1_text_4k",
-                                  "c2_bin_256", "c3_bin_64k", "c4_mixed", "c5_shard0", "c5_shard7"])
-def test_config_batches(ws, name):
+@pytest.mark.parametrize("name,mode", [(n, "fused") for n in [
+    "t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m", "c1_text_4k", "c2_bin_256", "c3_bin_64k",
+    "c4_mixed", "c5_shard0", "c5_shard7"]] + [(n, "runs1k") for n in [
+    "t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m"]])
+def test_config_batches(ws, name, mode):
     buf, c = tools_batch(name)
     assert dev_digest(buf) == c["in_digest"], "device generator disagrees with the host spec"
-    dec = ws.frame_decoder()
+    dec = ws.frame_decoder(**MODES[mode])
     r = dec.decode(buf, cap=16)
     assert r.nframes == c["decoded_frames"]
     assert dev_digest(buf) == c["out_digest"]

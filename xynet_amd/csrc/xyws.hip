@@ -13,8 +13,9 @@
 //                    boundary chase (exact, latency bound; debug/reference shape).
 //   k_unmask_tiles   step 2 of both: byte tiles of 16 KiB per workgroup, each
 //                    lane XORs 4 x 16 B with the covering frames' rotated keys.
-//   k_stream_fused   (xyws_stream.hip) the default stream decoder: one pass,
-//                    boundary discovery by tile + decoupled look-back.
+//   k_stream_runs    (xyws_stream.hip) the default stream decoder: one
+//                    workgroup per contiguous run, exact chase inside a run,
+//                    speculative run entries checked by the predecessor.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -366,7 +367,7 @@ int xyws_ctx_create(int device, xyws_ctx** out) {
   c->tab_mem = nullptr;
   c->tab_cap = 0;
   c->err = nullptr;
-  stream_scratch_init(&c->ss);
+  stream_scratch_init(&c->ss, device);
   if (hipMalloc(&c->err, 64) != hipSuccess) {
     delete c;
     return XYWS_ERR_NOMEM;

@@ -95,3 +95,45 @@ XYWS_DEV uint64_t sat_add(uint64_t a, uint64_t b) {
   uint64_t s = a + b;
   return s < a ? ~0ull : s;
 }
+
+// The same parse from 16 little-endian bytes held in four dwords w[0..3]
+// (byte i = w[i/4] >> 8*(i%4)), of which `avail` are valid: register-only,
+// no byte array (the kernels read headers as dwords from LDS or memory).
+XYWS_DEV hdr_info parse_header_words(const uint32_t w[4], uint32_t avail) {
+  hdr_info h;
+  h.plen = 0; h.key = 0; h.hlen = 0; h.flags = 0; h.status = 0;
+  if (avail < 2) return h;
+  const uint32_t b0 = w[0] & 0xFF, b1 = (w[0] >> 8) & 0xFF;
+  const uint32_t l7 = b1 & 0x7Fu;
+  const uint32_t ext = l7 == 126 ? 2u : (l7 == 127 ? 8u : 0u);
+  const uint32_t masked = b1 >> 7;
+  const uint32_t need = 2u + ext + 4u * masked;
+  if (avail < need) return h;
+  // bytes 2..9 as a big-endian length; bytes k..k+3 as the key (k = 2 + ext)
+  const uint64_t lo8 = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  const uint64_t hi8 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  const uint64_t b2_9 = (lo8 >> 16) | (hi8 << 48);  // bytes 2..9, little-endian
+  uint64_t len = l7;
+  if (ext == 2) len = ((b2_9 & 0xFF) << 8) | ((b2_9 >> 8) & 0xFF);
+  else if (ext == 8) len = __builtin_bswap64(b2_9);
+  uint32_t key = 0;
+  if (masked) {
+    const uint32_t k = 2 + ext;  // 2, 4 or 10
+    key = (k == 2) ? __builtin_amdgcn_alignbyte(w[1], w[0], 2)
+        : (k == 4) ? w[1] : __builtin_amdgcn_alignbyte(w[3], w[2], 2);
+  }
+  const uint32_t op = b0 & 0x0Fu;
+  uint8_t st = 0;
+  if (b0 & 0x70u) st |= XYWS_ST_RSV;
+  if ((op >= 3 && op <= 7) || op >= 11) st |= XYWS_ST_RESERVED_OPCODE;
+  if ((l7 == 126 && len < 126) || (l7 == 127 && len <= 0xFFFFull)) st |= XYWS_ST_NONMINIMAL_LENGTH;
+  if (l7 == 127 && (len >> 63)) st |= XYWS_ST_LENGTH_MSB;
+  if (op >= 8 && (!(b0 & 0x80u) || len > 125)) st |= XYWS_ST_BAD_CONTROL;
+  if (!masked) st |= XYWS_ST_UNMASKED;
+  h.plen = len;
+  h.key = key;
+  h.hlen = need;
+  h.flags = (uint8_t)(op | ((b0 & 0x80u) ? XYWS_FLAG_FIN : 0u) | (masked ? XYWS_FLAG_HAS_MASK : 0u));
+  h.status = st;
+  return h;
+}

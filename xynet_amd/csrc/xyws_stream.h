@@ -1,25 +1,29 @@
-// xyws_stream.h — fused single-pass stream decoder (xyws_stream.hip).
+// xyws_stream.h — run-parallel stream decoder (xyws_stream.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "xyws.h"
 
-// Scratch owned by a context: per-tile status words + records for the
-// decoupled look-back, the tile ticket counter and a device error word.
+// Scratch owned by a context: one record + one flag per run, a ticket and a
+// device error word.
 struct stream_scratch {
   void* mem;            // device allocation
   uint64_t bytes;
-  uint64_t max_tiles;   // tiles the allocation covers
+  uint64_t max_runs;    // runs the allocation covers
+  int ncu;              // compute units of the context's device (runs per launch)
 };
 
-void stream_scratch_init(stream_scratch* s);
+void stream_scratch_init(stream_scratch* s, int device);
 void stream_scratch_free(stream_scratch* s);
 int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes);
 uint32_t stream_scratch_error(stream_scratch* s);
 int stream_scratch_stats(stream_scratch* s, uint64_t out[32]);
 
-// Internal decode option: count resolution events (xyws_debug_stats).
-#define XYWS_OPT_STATS 0x100u  // synchronous read of the error word
+// Internal decode options (not part of include/xyws.h):
+#define XYWS_OPT_STATS 0x100u      // count speculation/repair events (xyws_debug_stats)
+#define XYWS_OPT_SMALL_SEG 0x200u  // 1 KiB segments, one per run: exercises run-boundary
+                                   // speculation and repair on small test inputs
+#define XYWS_OPT_NO_STORE 0x20000u // diagnostics: decode without writing (timing split only)
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
                         const xyws_carry* cin, xyws_carry* cout, xyws_frame* frames, uint64_t cap,
                         uint64_t* nframes, uint32_t opts, hipStream_t stream);

@@ -1,64 +1,53 @@
-// xyws_stream.hip — fused stream decoder for gfx950 (default mode of
-// xyws_decode_stream).
+// xyws_stream.hip — run-parallel stream decoder for gfx950 (the default mode
+// of xyws_decode_stream).
 //
-// Problem: in a back-to-back batch the start of frame k+1 is known only after
-// the header of frame k is parsed (websocket_frame_header.h:305-385 gives the
-// header size and the payload length), so frame boundaries form a linked list
-// through the batch. A serial chase from HBM costs one dependent load per
-// frame, far below the HBM roofline.
+// The problem: in a back-to-back batch the start of frame k+1 is known only
+// once the header of frame k is parsed (websocket_frame_header.h:305-385 gives
+// header size and payload length), so frame boundaries form a linked list
+// through the batch, and websocket_mask (websocket_frame_mask.h:6-25) can only
+// run on a payload once its frame is found.
 //
-// Geometry: a SEGMENT is 64 KiB; a persistent 512-thread workgroup takes
-// segments by atomic ticket and runs a two-stage software pipeline over them:
-// in each iteration it INDEXES its new segment t and then UNMASKS the segment
-// it indexed in the previous iteration. The lag of one index phase is what
-// lets the unmask stage run without waiting: by then every aggregate the
-// speculation needs has long been published.
+// Geometry (measured, scripts/bw_probe.hip): the in-place XOR of a 2 GiB batch
+// runs at 5.98 TB/s (R+W) with one 1024-thread workgroup per CU, each streaming
+// its own contiguous byte range in 128 KiB SEGMENTS staged in LDS, nontemporal
+// 16-byte buffer loads/stores and a one-segment register prefetch. This kernel
+// is that data movement plus the header chase:
 //
-// INDEX(t) — local work only, never waits:
-//  1. Load the segment (16 chunks of 16 B per lane, buffer descriptor with
-//     base and range in SGPRs). For each 16 KiB sub-tile: stage it (+16 B
-//     halo) in LDS, SWAR-prefilter every byte position for a plausible client
-//     header (RSV = 0, known opcode, MASK as expected), check each candidate's
-//     successor (position + header + length) is itself a candidate, and append
-//     the survivors in position order.
-//  2. Link survivors (successor = survivor at pos + H + len, EXIT past the
-//     segment, DEAD otherwise); pointer doubling gives every node its 2^b-th
-//     successors, its frame count to the chain end and its chain end.
-//  3. Publish the AGGREGATE record: the first 16 nodes whose chain leaves the
-//     segment (position, outcome, count), up to 8 outcomes (exit, last frame),
-//     and the first 32 bytes of the segment (headers straddling into it are
-//     read from this copy: the bytes themselves may be unmasked meanwhile).
-// UNMASK(k):
-//  4. Input state by speculation over the aggregates of the 63 preceding
-//     segments: an entry node is trusted when some outcome of an earlier
-//     segment (or the batch start) exits exactly onto it ("link support"); k
-//     takes the trusted outcome of the nearest segment that reaches it.
-//     Without one, it takes the nearest published output that reaches it.
-//  5. Own frames from that input: the path from the entry survivor through
-//     the jump tables (binary lifting, one frame per thread), or an exact
-//     header chase. Publish (assumed input, output); the second of segments
-//     k-1 and k to publish compares k's input with k-1's output ("pair").
-//  6. XOR words for every chunk from the frame list, then load, XOR, store
-//     the chunks that change (one read and one write of the payload; the
-//     re-read of the lagged segment is served by the Infinity Cache).
-// Validation is deferred: segment 0's input is exact, so when every pair
-// matches, every input is exact by induction. The last workgroup to exit
-// checks that; on a mismatch it repairs in order from the first bad pair:
-// undo the wrong frames (XOR is an involution; a wrong chain never XORs its
-// own header bytes, so it is re-derived from the bytes as they stand), redo
-// with the exact input, until inputs match again. Speculation decides speed
-// only; any byte stream (RSV bits, reserved opcodes, unmasked or non-minimal
-// frames) decodes exactly as the reference parses it.
+//  * The batch is cut into RUNS of whole segments, one per workgroup (a ticket
+//    gives runs out in dispatch order).
+//  * Inside a run the chase is EXACT and serial: lane 0 parses each header from
+//    the LDS copy of the segment and appends (payload range, rotated key word) to
+//    a frame list; then every lane XORs its 16-byte chunks with the listed keys
+//    and stores them. No speculation, no waiting, inside a run.
+//  * A run r > 0 does not know where the chain enters it. Its prologue takes the
+//    earliest position whose chain of KHDR headers is plausible for a client
+//    stream (RSV = 0, known opcode, control frames short with FIN, MASK as
+//    expected, minimal length encoding) and publishes it as h_r (for a 7-bit
+//    length form, the next node instead: a false short "header" just before a
+//    true one lands exactly on it, the next node is then true either way), with
+//    its write start W_r = round16(h_r + header). Run r writes bytes >= W_r,
+//    run r-1 writes bytes < W_r: run r-1 keeps chasing past its range until its
+//    exact chain reaches h_r and XORs the bytes up to W_r. If its chain lands
+//    exactly on h_r, run r's entry is exact; by induction from run 0 (exact:
+//    batch start and carry) every run is exact when every boundary matches.
+//  * A mismatch (rare: an implausible true header, or a plausible false chain)
+//    is repaired by k_stream_finish: undo the mis-speculated run (replaying its
+//    own chain XORs its payloads back; a chain never writes its own headers),
+//    then redo its range from the exact chain, boundary after boundary until the
+//    chains agree again. Speculation decides speed only: any byte stream (RSV
+//    bits, reserved opcodes, unmasked or non-minimal frames, random bytes)
+//    decodes exactly as the reference parses it.
 //
-// Inter-workgroup hand-off follows MI355X_MICROARCH.md §Workgroup dispatch:
-// record words are written with agent-scope (sc1) stores, drained with
-// s_waitcnt vmcnt(0), then an sc1 flag store or agent-scope atomic; readers
-// poll with sc1 loads. Flags and counters are zeroed by hipMemsetAsync before
-// every launch. Every spin is bounded and reports through the device error
-// word. Deadlock freedom: every wait points to a segment whose ticket was
-// taken earlier (or to k+1, whose ticket was taken before this workgroup's
-// current one), and the holder of such a ticket runs its index phase before
-// anything that can wait.
+// The only inter-workgroup hand-off is a run's published (h, W): sc1 record
+// stores, s_waitcnt vmcnt(0), one agent-scope flag store; the reader polls the
+// flag with sc1 loads and reads the record with sc1 loads
+// (MI355X_MICROARCH.md §Workgroup dispatch, valid forms). A run waits only for
+// the prologue of the next run with an entry, whose ticket was taken after its
+// own and which never waits, so the lowest ticket always progresses. Header
+// bytes are read only where no other workgroup writes: below the successor's W
+// (a header that would cross it stops the chase, "cut"), or in the run's own
+// range. Flags and the ticket are zeroed by hipMemsetAsync before every launch;
+// spins are bounded and report through the device error word.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -67,141 +56,87 @@
 
 namespace {
 
-constexpr uint32_t SEG = 65536;            // segment bytes
-constexpr uint32_t SUB = 8192;             // sub-tile bytes staged in LDS
-constexpr uint32_t NSUB = SEG / SUB;       // 8
-constexpr uint32_t NT = 256;               // threads per workgroup (4 waves)
-constexpr uint32_t NW = NT / 64;           // waves per workgroup
-constexpr uint32_t CHS = SEG / (16 * NT);  // 16 chunks of 16 B per lane
-constexpr uint32_t CHSUB = SUB / (16 * NT);  // 2 per sub-tile
-constexpr uint32_t PPL = SUB / NT;         // prefilter positions per lane (32)
-constexpr uint32_t HALO = 16;
-constexpr uint32_t SMAX = 512;             // survivors tracked per segment
-constexpr uint32_t LV = 9;                 // jump-table levels: 2^LV >= SMAX
-constexpr uint32_t NPT = SMAX / NT;        // survivor nodes per thread (2)
-constexpr uint32_t FCAP = SUB / 16;        // frame-list entries per pass (overlays the sub-tile)
-constexpr uint32_t NENT = 16;              // aggregate entry nodes (2 per record word)
-constexpr uint32_t NOUT = 8;               // aggregate outcomes (2 record words each)
-constexpr uint32_t SPIN = 1u << 24;        // bounded spins (~1 s)
-constexpr uint32_t WIN = 64;               // segments seen by one speculation (one per lane)
-constexpr uint32_t BKT = 8;                // exits kept per target segment during speculation
-constexpr uint32_t OOB = 0x80000000u;      // buffer offset past every range: load 0, store dropped
+constexpr uint64_t NONE = ~0ull;
+constexpr uint32_t FCAP = 512;        // frame-list entries per pass
+constexpr uint32_t PAD = 32;          // LDS bytes after the segment (5-dword header reads)
+// Headers a speculative entry's chain must pass, by the entry's length form:
+// a false 127-form header needs 0xFF/0x7F plus an 8-byte length below 2^46
+// (~5e-10 per random position), a 126-form one 0xFE/0x7E (~1.4e-4), a 7-bit
+// one just a plausible first byte (~1.7e-2); each further plausible header
+// multiplies by ~1.8e-2. Short hops mostly stay in LDS; long ones are memory reads.
+constexpr uint32_t KHDR_127 = 2, KHDR_126 = 4, KHDR_7 = 6;
+constexpr uint32_t SPIN = 1u << 24;   // bounded spins (s_sleep 2 each: ~1 s)
+constexpr uint32_t OOB = 0x80000000u; // buffer offset past every range: load 0, store dropped
+constexpr int AUX_NT = 2;             // buffer cache policy: nontemporal
+constexpr uint64_t PLEN_SPEC_MAX = 1ull << 46;
+constexpr uint32_t MAX_RUNS = 1024;
+constexpr uint32_t RUNS_PER_CU = 2;   // workgroups resident per CU (LDS: two ~72 KiB blocks)
 
-constexpr uint16_t N_EXIT = 0xFFFF, N_DEAD = 0xFFFE;
-constexpr uint8_t O_DEAD = 0xFE, O_UNREC = 0xFD;  // node outcome marks
-constexpr uint16_t J_TERM = 0xFFFF;        // jump past the end of a chain
-constexpr uint16_t T_DEAD = 0xFFFF;        // chain ends in a dead end
-
-// composition-state bits
-constexpr uint32_t S_PARTIAL = 1;    // stream ended in an incomplete header at X
+// chase-state bits
+constexpr uint32_t S_PARTIAL = 1;    // header at X incomplete at the batch end
 constexpr uint32_t S_NOCOV = 2;      // no frame covers the bytes before X
 constexpr uint32_t S_CARRIED = 4;    // covering frame = the open frame carried in
 constexpr uint32_t S_HDRCARRY = 8;   // covering frame's header began in the previous batch
 constexpr uint32_t S_PARTCARRY = 16; // the carried partial header is still incomplete
-constexpr uint32_t S_KEEP = S_NOCOV | S_CARRIED | S_HDRCARRY;
+constexpr uint32_t S_CUT = 32;       // header at X crosses the write limit (left to the repair)
 
-// record layout: R_WORDS x u64 per segment
-enum {
-  R_META = 0,   // n_entries | n_outcomes << 8 | overflow << 16
-  R_ENT0 = 1,   // NENT entries, two per word: pos (16) | rem (13) << 16 | outcome (3) << 29
-  R_OUT0 = 9,   // NOUT outcomes x 2 words: exit; cov_ps - ss (20) | hlen (4) << 20 | kw << 32
-  R_CI = 25,    // assumed input state (X, cov_ps, cov_start, kw | st << 32)
-  R_CO = 29,    // output state computed from it
-  R_NA = 33,    // frames whose header starts in the segment (given the input)
-  R_NI = 34,    // inclusive frame-count prefix (descriptor ordinals)
-  R_HEAD = 35,  // the segment's first 32 bytes as indexed (4 words)
-  R_WORDS = 40
+template <uint32_t NT_, uint32_t CH_>
+struct geom {
+  static constexpr uint32_t NT = NT_, CH = CH_, SEG = NT_ * CH_ * 16;
 };
+using G_PROD = geom<512, 8>;   // 64 KiB segments, 8 waves, two workgroups per CU
+using G_SMALL = geom<64, 1>;   // 1 KiB segments, one wave (XYWS_OPT_SMALL_SEG)
 
 struct fent {
-  uint32_t start, ps, end, kw;  // segment-relative; ps/end clamped to [0, 2^32-1]
+  uint32_t start, ps, end, kw;  // segment-relative, clamped to [0, 2^32-1]
 };
 
 struct cstate {
-  uint64_t X;          // first frame start >= current position (absolute)
-  uint64_t cov_ps;     // payload start of the frame ending at X
-  uint64_t cov_start;  // header start of that frame
-  uint64_t cnt;        // frames whose header completed before X
-  uint32_t cov_kw;     // aligned key word of that frame
+  uint64_t X;          // next frame start (absolute)
+  uint64_t cov_ps;     // payload start of the frame covering the bytes before X
+  uint64_t cov_start;  // its header start
+  uint32_t cov_kw;     // its aligned key word
+  uint32_t cov_key;    // its key (wire order)
   uint32_t st;         // S_* bits
+  uint32_t pad;
 };
 
-// Survivors of one indexed segment, kept in LDS until its unmask stage.
-struct sv_buf {
-  uint32_t pos[SMAX];      // segment-relative position
-  uint32_t nrel[SMAX];     // successor position (segment-relative, saturating)
-  uint32_t key[SMAX];
-  uint16_t jmp[LV][SMAX];  // jmp[b][i]: the 2^b-th successor of i (J_TERM past the chain end)
-  uint16_t rem[SMAX];      // frames from this node to the chain end
-  uint8_t out[SMAX];       // outcome id / O_* mark
-  uint8_t hlen[SMAX];
-  uint64_t outs[NOUT][4];  // outcomes: exit, cov_ps, cov_start, kw
-  uint64_t seg;
-  uint32_t nsurv, overflow;
+// run record: R_WORDS x u64
+enum {
+  R_H = 0, R_W, R_S0, R_HEAD = R_S0 + 5,            // prologue: entry, write start, state, head frames
+  R_OK = 8, R_HN, R_WN, R_CNT, R_TAIL, R_FIRST,     // results (R_OK: ok | succ << 32)
+  R_F0 = 14,                                        // final state (5 words)
+  R_EFROM = 20, R_ECNT, R_EORD, R_ECARRY,           // emission plan (k_stream_finish)
+  R_WORDS = 24
 };
 
-struct __attribute__((aligned(16))) st_lds {
-  union {
-    uint8_t sub[SUB + HALO];  // index: sub-tile bytes
-    fent flist[FCAP];         // unmask: frame list
-  };
-  uint32_t bits[SUB / 32];    // candidate bitmap of the current sub-tile
-  uint16_t nxt[SMAX];         // index: successor survivor / N_EXIT / N_DEAD
-  uint16_t last[SMAX];        // index: chain end (T_DEAD: dead end)
-  sv_buf sv;
-  uint32_t scan[8];
-  uint32_t ents[NENT];
-  uint32_t bk_n[WIN];         // speculation: exits landing in each window segment
-  uint32_t bk[WIN][BKT];
-  uint64_t seg_id, chase_X, fbase, nbase;
-  cstate in, out;
-  uint64_t tstamp;            // wave 0's last s_memtime stamp (stats builds)
-  uint32_t nfl, pass_done, nent_pub, nout_pub, mode, node_x, rem_x, red;
-};
-
-struct st_params {
+struct run_params {
   uint8_t* base;
-  uint64_t lo, hi, nseg;
+  uint64_t lo, hi;
+  uint64_t nseg;          // segments covering [0, hi)
+  uint32_t nruns, spr;    // runs, segments per run
   const xyws_carry* cin;  // private snapshot of the incoming carry
   xyws_carry* cout;
   xyws_frame* frames;
   uint64_t cap;
   uint64_t* nframes;
-  uint32_t* head;   // [0] ticket, [1] error word, [2] exited workgroups, [3] bad pair seen,
-                    // [4..5] u64 frame total
-  uint32_t* fA;     // per segment: aggregate published
-  uint32_t* fC;     // per segment: (assumed input, output) published
-  uint32_t* fN;     // per segment: 1 = count, 2 = inclusive count prefix
-  uint32_t* fP;     // per segment: 1 = input == predecessor's output, 2 = not
-  uint64_t* recs;   // R_WORDS per segment
+  uint64_t* rec;          // R_WORDS per run
+  uint32_t* flags;        // per run: 1 = prologue published
+  uint32_t* head;         // [0] ticket, [1] error word, [2..3] u64 total; stats at [32..)
   uint32_t opts;
 };
 
-// The workgroup's LDS block and the launch parameters, reachable from every
-// stage function without passing pointers: a pointer parameter would be a
-// generic address, turning every LDS access into a flat instruction that also
-// waits on outstanding global loads. Parameters are read through the kernarg
-// segment (scalar loads).
-__shared__ st_lds g_L;
-typedef const __attribute__((address_space(4))) st_params kparams_t;
-XYWS_DEV st_params kparams() {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return *(kparams_t*)(__builtin_amdgcn_kernarg_segment_ptr());
-#else
-  return st_params{};
-#endif
-}
+template <class G>
+struct __attribute__((aligned(16))) lds_t {
+  uint8_t seg[G::SEG + PAD];
+  fent fl[FCAP];
+  cstate S;
+  cstate B;  // k_stream_finish: exact state handed to a repaired run
+  uint64_t hn, Wn, succ, first_after, cnt, tail, aux0, aux1, aux2, bcnt, bfirst;
+  uint32_t nfl, pass_hi, known, past, ok, done, end, best, ticket, act, repaired;
+};
 
-// ---------------------------------------------------------------- debug counters
-// With XYWS_OPT_STATS the kernel counts resolution events and per-phase
-// s_memtime cycles into the stats area (read back by xyws_debug_stats).
-enum { ST_EXACT_IN = 0, ST_SPEC, ST_FALLBACK, ST_BADPAIR, ST_REPAIR, ST_MODE1, ST_MODE2,
-       ST_NSURV, ST_OVERFLOW, ST_SEGS,
-       ST_T_INDEX = 16, ST_T_LINK, ST_T_INPUT, ST_T_CHAIN, ST_T_LIST, ST_T_APPLY,
-       ST_F_ISSUE = 24, ST_F_HEAD, ST_F_POLL, ST_F_RECS, ST_F_STAGE0, ST_F_PREAPPLY, ST_F_ACCUM,
-       ST_NSTAT = 32 };
-
-// ---------------------------------------------------------------- hand-off
+// ---------------------------------------------------------------- small helpers
 XYWS_DEV void st_store(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -211,1049 +146,798 @@ XYWS_DEV uint64_t st_load(const uint64_t* p) {
 XYWS_DEV uint32_t flag_load(const uint32_t* p) {
   return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-XYWS_DEV void flag_publish(uint32_t* p, uint32_t v) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // record stores drained before the flag
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-XYWS_DEV bool stat_on(const st_params& P) { return (P.opts & XYWS_OPT_STATS) != 0; }
-XYWS_DEV void stat_add(const st_params& P, uint32_t i, uint64_t v) {
-  if (__builtin_amdgcn_mbcnt_lo(~0u, 0) == 0)  // one lane
-    atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + i, (unsigned long long)v);
-}
-XYWS_DEV void stat_phase(const st_params& P, uint32_t i, uint64_t& t) {
-  if (!stat_on(P)) return;
-  const uint64_t now = __builtin_amdgcn_s_memtime();
-  stat_add(P, i, now - t);
-  t = now;
-}
-XYWS_DEV void spin_for(const uint32_t* p, uint32_t want, uint32_t* err, uint32_t code) {
-  for (uint32_t it = 0; it < SPIN; it++) {
-    if (flag_load(p) >= want) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      return;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  atomicOr(err, code);
+XYWS_DEV bool stats_on(const run_params& P) { return (P.opts & XYWS_OPT_STATS) != 0; }
+enum { ST_RUNS = 0, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRAMES,
+       ST_T_PRO = 16, ST_T_MAIN, ST_T_WAIT, ST_T_FILL, ST_T_CHASE, ST_T_XOR, ST_T_TAIL, ST_T_PF, ST_T_CP };
+XYWS_DEV void stat_add(const run_params& P, uint32_t i, uint64_t v) {
+  if (stats_on(P)) atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + i, (unsigned long long)v);
 }
 
-// ---------------------------------------------------------------- parsing
-// Header from 16 little-endian bytes held in four dwords w[0..3] (byte i =
-// w[i/4] >> 8*(i%4)), of which `avail` are valid. Same semantics as
-// parse_header_bytes (websocket_frame_header.h:305-385).
-XYWS_DEV hdr_info parse_header_words(const uint32_t w[4], uint32_t avail) {
+XYWS_DEV uint32_t clamp_rel(uint64_t x, uint64_t ss) {
+  if (x <= ss) return 0;
+  const uint64_t d = x - ss;
+  return d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+}
+
+XYWS_DEV void put_state(uint64_t* r, const cstate& s) {
+  st_store(r + 0, s.X);
+  st_store(r + 1, s.cov_ps);
+  st_store(r + 2, s.cov_start);
+  st_store(r + 3, (uint64_t)s.cov_kw | ((uint64_t)s.cov_key << 32));
+  st_store(r + 4, s.st);
+}
+XYWS_DEV cstate get_state(const uint64_t* r) {
+  cstate s;
+  s.X = st_load(r + 0);
+  s.cov_ps = st_load(r + 1);
+  s.cov_start = st_load(r + 2);
+  const uint64_t k = st_load(r + 3);
+  s.cov_kw = (uint32_t)k;
+  s.cov_key = (uint32_t)(k >> 32);
+  s.st = (uint32_t)st_load(r + 4);
+  s.pad = 0;
+  return s;
+}
+XYWS_DEV cstate frame_state(uint64_t start, const hdr_info& h) {
+  cstate s;
+  s.cov_start = start;
+  s.cov_ps = start + h.hlen;
+  s.X = sat_add(s.cov_ps, h.plen);
+  s.cov_key = h.key;
+  s.cov_kw = aligned_key(h.key, s.cov_ps, 0);
+  s.st = 0;
+  s.pad = 0;
+  return s;
+}
+
+// ---------------------------------------------------------------- header reads
+// Header at absolute x from memory, using only bytes below lim (and hi).
+XYWS_DEV hdr_info hdr_global(const run_params& P, uint64_t x, uint64_t lim) {
   hdr_info h;
   h.plen = 0; h.key = 0; h.hlen = 0; h.flags = 0; h.status = 0;
-  if (avail < 2) return h;
-  const uint32_t b0 = w[0] & 0xFF, b1 = (w[0] >> 8) & 0xFF;
-  const uint32_t l7 = b1 & 0x7Fu;
-  const uint32_t ext = l7 == 126 ? 2u : (l7 == 127 ? 8u : 0u);
-  const uint32_t masked = b1 >> 7;
-  const uint32_t need = 2u + ext + 4u * masked;
-  if (avail < need) return h;
-  // bytes 2..9 as a big-endian length; bytes k..k+3 as the key (k = 2 + ext)
-  const uint64_t lo8 = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-  const uint64_t hi8 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
-  const uint64_t b2_9 = (lo8 >> 16) | (hi8 << 48);  // bytes 2..9, little-endian
-  uint64_t len = l7;
-  if (ext == 2) len = ((b2_9 & 0xFF) << 8) | ((b2_9 >> 8) & 0xFF);
-  else if (ext == 8) len = __builtin_bswap64(b2_9);
-  uint32_t key = 0;
-  if (masked) {
-    const uint32_t k = 2 + ext;  // 2, 4 or 10
-    key = (k == 2) ? __builtin_amdgcn_alignbyte(w[1], w[0], 2)
-        : (k == 4) ? w[1] : __builtin_amdgcn_alignbyte(w[3], w[2], 2);
-  }
-  const uint32_t op = b0 & 0x0Fu;
-  uint8_t st = 0;
-  if (b0 & 0x70u) st |= XYWS_ST_RSV;
-  if ((op >= 3 && op <= 7) || op >= 11) st |= XYWS_ST_RESERVED_OPCODE;
-  if ((l7 == 126 && len < 126) || (l7 == 127 && len <= 0xFFFFull)) st |= XYWS_ST_NONMINIMAL_LENGTH;
-  if (l7 == 127 && (len >> 63)) st |= XYWS_ST_LENGTH_MSB;
-  if (op >= 8 && (!(b0 & 0x80u) || len > 125)) st |= XYWS_ST_BAD_CONTROL;
-  if (!masked) st |= XYWS_ST_UNMASKED;
-  h.plen = len;
-  h.key = key;
-  h.hlen = need;
-  h.flags = (uint8_t)(op | ((b0 & 0x80u) ? XYWS_FLAG_FIN : 0u) | (masked ? XYWS_FLAG_HAS_MASK : 0u));
-  h.status = st;
-  return h;
-}
-
-// Header at absolute position p. Bytes of p's own segment come from global
-// memory (a chain's header bytes are never XORed by that chain); bytes past
-// the segment end come from the next segment's published first 32 bytes, as
-// they were before anyone unmasked that segment.
-XYWS_DEV hdr_info header_safe(const st_params& P, uint64_t p) {
-  const uint64_t se = (p / SEG + 1) * SEG;
-  const uint64_t a = p & ~3ull;
-  const uint32_t sh = (uint32_t)(p & 3);
+  const uint64_t top = lim < P.hi ? lim : P.hi;
+  if (x >= top) return h;
+  const uint64_t a = x & ~3ull;
+  const uint32_t sh = (uint32_t)(x & 3);
+  const uint64_t dl = (P.hi + 3) & ~3ull;  // dwords wholly or partly inside the batch
   uint32_t r[5];
 #pragma unroll
   for (int i = 0; i < 5; i++) {
     const uint64_t q = a + 4 * i;
-    uint32_t v = 0;
-    if (q < P.hi) {
-      if (q < se) {
-        v = *reinterpret_cast<const uint32_t*>(P.base + q);
-      } else {
-        const uint64_t w = st_load(P.recs + (se / SEG) * R_WORDS + R_HEAD + ((q - se) >> 3));
-        v = (uint32_t)(w >> (((q - se) & 4) * 8));
-      }
-    }
-    r[i] = v;
+    r[i] = q < dl ? *reinterpret_cast<const uint32_t*>(P.base + q) : 0u;
   }
+  // wait here (vmcnt 0, other counters untouched) so that no register leaves
+  // this branch with a load pending: otherwise the compiler's wait lands after
+  // the join with the LDS path and every header parse waits for the segment
+  // prefetch in flight
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   uint32_t w[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) w[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
-  const uint64_t room = P.hi > p ? P.hi - p : 0;
+  const uint64_t room = top - x;
   return parse_header_words(w, room < 16 ? (uint32_t)room : 16u);
 }
 
-// Header whose first h0 bytes were carried from the previous batch.
-XYWS_DEV hdr_info header_carried(const uint8_t* base, uint64_t lo, uint64_t hi, const xyws_carry* c) {
-  uint8_t hb[XYWS_MAX_FRAME_HEADER_SIZE];
+// Header at absolute x: from the LDS copy of segment [ss, ss+SEG) when all 14
+// possible bytes lie in it, else from memory.
+template <class G>
+XYWS_DEV hdr_info hdr_at(const run_params& P, const lds_t<G>& L, uint64_t ss, uint64_t x, uint64_t lim) {
+  const uint64_t top = lim < P.hi ? lim : P.hi;
+  if (x >= ss && x - ss + XYWS_MAX_FRAME_HEADER_SIZE <= G::SEG && x < top) {
+    const uint32_t o = (uint32_t)(x - ss), a = o & ~3u, sh = o & 3u;
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(L.seg + a);
+    const uint32_t r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+    uint32_t w[4];
+    w[0] = __builtin_amdgcn_alignbyte(r1, r0, sh);
+    w[1] = __builtin_amdgcn_alignbyte(r2, r1, sh);
+    w[2] = __builtin_amdgcn_alignbyte(r3, r2, sh);
+    w[3] = __builtin_amdgcn_alignbyte(r4, r3, sh);
+    const uint64_t room = top - x;
+    return parse_header_words(w, room < 16 ? (uint32_t)room : 16u);
+  }
+  return hdr_global(P, x, lim);
+}
+
+// Header whose first h0 bytes were carried from the previous batch (the rest
+// from the batch start), assembled in registers.
+XYWS_DEV hdr_info header_carried(const run_params& P) {
+  const xyws_carry* c = P.cin;
   const uint32_t h0 = c->hdr_len < XYWS_MAX_FRAME_HEADER_SIZE ? c->hdr_len : XYWS_MAX_FRAME_HEADER_SIZE;
-  uint32_t n = 0;
-  for (; n < h0; n++) hb[n] = c->hdr[n];
-  for (; n < XYWS_MAX_FRAME_HEADER_SIZE && lo + (n - h0) < hi; n++) hb[n] = base[lo + (n - h0)];
-  return parse_header_bytes(hb, n);
+  uint32_t w[4] = {0u, 0u, 0u, 0u}, n = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < XYWS_MAX_FRAME_HEADER_SIZE; i++) {
+    uint32_t b = 0;
+    bool have = true;
+    if (i < h0) b = c->hdr[i];
+    else if (P.lo + (i - h0) < P.hi) b = P.base[P.lo + (i - h0)];
+    else have = false;
+    if (have && n == i) {
+      w[i >> 2] |= b << (8u * (i & 3u));
+      n++;
+    }
+  }
+  return parse_header_words(w, n);
 }
 
-XYWS_DEV hdr_info header_lds(const uint8_t* sub, uint32_t prel, uint64_t pabs, uint64_t hi) {
-  const uint32_t a = prel & ~3u, sh = prel & 3u;
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(sub + a);
-  uint32_t w[4];
-  const uint32_t r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
-  w[0] = __builtin_amdgcn_alignbyte(r1, r0, sh);
-  w[1] = __builtin_amdgcn_alignbyte(r2, r1, sh);
-  w[2] = __builtin_amdgcn_alignbyte(r3, r2, sh);
-  w[3] = __builtin_amdgcn_alignbyte(r4, r3, sh);
-  const uint64_t room = hi > pabs ? hi - pabs : 0;
-  return parse_header_words(w, room < 16 ? (uint32_t)room : 16u);
-}
-
-// Conformance filter of a fully parsed header (speculation only).
-XYWS_DEV bool plausible(const hdr_info& h, uint8_t b1) {
+// A header a client stream plausibly holds (speculation only).
+XYWS_DEV bool plausible(const hdr_info& h, bool unmasked) {
   if (!h.hlen) return false;
-  const uint32_t op = h.flags & 0x0F;
-  if (op >= 8 && (!(h.flags & XYWS_FLAG_FIN) || h.plen > 125)) return false;
-  const uint32_t l7 = b1 & 0x7F;
-  if (l7 == 126 && h.plen < 126) return false;
-  if (l7 == 127 && (h.plen <= 0xFFFF || (h.plen >> 62))) return false;
-  return true;
+  if (h.status & (XYWS_ST_RSV | XYWS_ST_RESERVED_OPCODE | XYWS_ST_NONMINIMAL_LENGTH |
+                  XYWS_ST_LENGTH_MSB | XYWS_ST_BAD_CONTROL))
+    return false;
+  if (((h.status & XYWS_ST_UNMASKED) != 0) != unmasked) return false;
+  return h.plen < PLEN_SPEC_MAX;
 }
 
-XYWS_DEV uint32_t clamp_rel(uint64_t x, uint64_t ts) {
-  if (x <= ts) return 0;
-  const uint64_t d = x - ts;
-  return d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+// Four candidate bits (bytes 0..3 of w) for a client header: RSV = 0, opcode in
+// {0,1,2} or {8,9,10} with FIN, MASK bit (first bit of the next byte) as
+// expected. A superset of plausible().
+XYWS_DEV uint32_t cand_nibble(uint32_t w, uint32_t wn, bool unmasked) {
+  const uint32_t b1s = (w >> 8) | (wn << 24);  // byte t = byte t+1
+  const uint32_t rsv_ok = ~((w & 0x70707070u) + 0x70707070u) & 0x80808080u;
+  const uint32_t bad = ((w << 5) | ((w << 6) & (w << 7)) | ((w << 4) & ~w)) & 0x80808080u;
+  const uint32_t m_ok = (unmasked ? ~b1s : b1s) & 0x80808080u;
+  const uint32_t c = rsv_ok & ~bad & m_ok;
+  return ((c >> 7) & 1u) | ((c >> 14) & 2u) | ((c >> 21) & 4u) | ((c >> 28) & 8u);
 }
 
-// State before the first byte of the batch (the output of "segment -1"),
-// from the carry snapshot.
-XYWS_DEV cstate initial_state(const st_params& P) {
+// State before the first byte of the batch, from the carry snapshot; cnt =
+// frames it completes (the carried-header frame).
+XYWS_DEV cstate initial_state(const run_params& P, uint64_t& cnt) {
   cstate s;
-  s.X = P.lo; s.cov_ps = P.lo; s.cov_start = P.lo; s.cnt = 0; s.cov_kw = 0; s.st = S_NOCOV;
+  s.X = P.lo; s.cov_ps = P.lo; s.cov_start = P.lo; s.cov_kw = 0; s.cov_key = 0; s.st = S_NOCOV; s.pad = 0;
+  cnt = 0;
   const xyws_carry* c = P.cin;
   const uint64_t R = c->payload_remaining;
   if (R) {
     const uint32_t k = (uint32_t)c->key[0] | ((uint32_t)c->key[1] << 8) |
                        ((uint32_t)c->key[2] << 16) | ((uint32_t)c->key[3] << 24);
     s.X = sat_add(P.lo, R);
-    s.cov_ps = P.lo;
     s.cov_kw = aligned_key(k, P.lo, c->phase);
+    s.cov_key = k;
     s.st = S_CARRIED;
     return s;
   }
-  const uint32_t h0 = c->hdr_len;
-  if (h0) {
-    hdr_info h = header_carried(P.base, P.lo, P.hi, c);
+  if (c->hdr_len) {
+    const hdr_info h = header_carried(P);
     if (!h.hlen) {  // still incomplete: the whole batch belongs to the header
       s.st = S_NOCOV | S_PARTIAL | S_PARTCARRY;
       return s;
     }
-    s.cov_start = P.lo;
-    s.cov_ps = P.lo + (h.hlen - h0);
+    s = frame_state(P.lo, h);
+    s.cov_ps = P.lo + (h.hlen - c->hdr_len);
     s.X = sat_add(s.cov_ps, h.plen);
     s.cov_kw = aligned_key(h.key, s.cov_ps, 0);
-    s.cnt = 1;
     s.st = S_HDRCARRY;
+    cnt = 1;
   }
   return s;
 }
 
-XYWS_DEV cstate load_state(const uint64_t* r) {
-  cstate s;
-  uint64_t w[4];
+// ---------------------------------------------------------------- segment I/O
+template <class G>
+XYWS_DEV __amdgpu_buffer_rsrc_t seg_rsrc(const run_params& P, uint64_t s) {
+  // [ss, ss + min(SEG, round16(hi) - ss)): loads past the batch read zero
+  const uint64_t ss = s * G::SEG, top = (P.hi + 15) & ~15ull;
+  const uint64_t room = top > ss ? top - ss : 0;
+  const uint32_t n = room >= G::SEG ? G::SEG : (uint32_t)room;
+  return __builtin_amdgcn_make_buffer_rsrc(P.base + ss, 0, n, 0x00020000);
+}
+
+template <class G>
+struct seg_io {
+  u32x4 e[G::CH];
+  uint64_t pf = NONE;  // segment whose loads are in e
+  XYWS_DEV void issue(const run_params& P, uint64_t s, uint32_t tid) {
+    const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, s);
 #pragma unroll
-  for (int i = 0; i < 4; i++) w[i] = st_load(r + i);
-  s.X = w[0]; s.cov_ps = w[1]; s.cov_start = w[2];
-  s.cov_kw = (uint32_t)w[3]; s.st = (uint32_t)(w[3] >> 32); s.cnt = 0;
-  return s;
-}
-
-XYWS_DEV void store_state(uint64_t* r, const cstate& s) {
-  st_store(r + 0, s.X);
-  st_store(r + 1, s.cov_ps);
-  st_store(r + 2, s.cov_start);
-  st_store(r + 3, (uint64_t)s.cov_kw | ((uint64_t)s.st << 32));
-}
-
-XYWS_DEV bool same_state(const cstate& a, const cstate& b) {
-  return a.X == b.X && a.cov_ps == b.cov_ps && a.cov_start == b.cov_start &&
-         a.cov_kw == b.cov_kw && a.st == b.st;
-}
-
-XYWS_DEV const uint64_t* rec_of(const st_params& P, uint64_t k) { return P.recs + k * R_WORDS; }
-
-// Exact chase by header reads from s.X while s.X < lim.
-XYWS_DEV void chase_global(const st_params& P, cstate& s, uint64_t lim) {
-  const uint64_t stop = lim < P.hi ? lim : P.hi;
-  for (;;) {
-    if ((s.st & S_PARTIAL) || s.X >= stop) return;
-    hdr_info h = header_safe(P, s.X);
-    if (!h.hlen) { s.st = (s.st & S_KEEP) | S_PARTIAL; return; }
-    s.cov_start = s.X;
-    s.cov_ps = s.X + h.hlen;
-    s.cov_kw = aligned_key(h.key, s.cov_ps, 0);
-    s.X = sat_add(s.cov_ps, h.plen);
-    s.cnt++;
-    s.st = 0;
+    for (uint32_t k = 0; k < G::CH; k++)
+      e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16u, k * G::NT * 16u, AUX_NT);
+    pf = s;
   }
-}
-
-// ---------------------------------------------------------------- wave/block helpers
-XYWS_DEV uint32_t rl32(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
-XYWS_DEV uint64_t rl64(uint64_t v, uint32_t l) {
-  return ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32) | rl32((uint32_t)v, l);
-}
-XYWS_DEV void wave_sync() {  // order this wave's LDS accesses across lanes
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// Block-wide exclusive scan of one value per thread (all threads call).
-XYWS_DEV uint32_t block_scan(st_lds& L, uint32_t v, uint32_t lane, uint32_t wave, uint32_t& total) {
-  uint32_t x = v;
+  // segment s into LDS (caller syncs before and after)
+  XYWS_DEV void fill(const run_params& P, lds_t<G>& L, uint64_t s, uint32_t tid) {
+    if (pf != s) issue(P, s, tid);
 #pragma unroll
-  for (uint32_t o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
+    for (uint32_t k = 0; k < G::CH; k++)
+      *reinterpret_cast<u32x4*>(&L.seg[(k * G::NT + tid) * 16u]) = e[k];
+    pf = NONE;
   }
-  __syncthreads();
-  if (lane == 63) L.scan[wave] = x;
-  __syncthreads();
-  uint32_t wb = 0, tot = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < NW; i++) {
-    const uint32_t si = L.scan[i];
-    if (i < wave) wb += si;
-    tot += si;
-  }
-  total = tot;
-  return wb + x - v;
-}
-
-// ---------------------------------------------------------------- resolution
-// Fallback input of segment k (no trusted speculation): the output of the
-// nearest segment that has published one, when it is k-1's or reaches k
-// (every segment in between is then covered by its last frame); otherwise
-// wait for the segments in between.
-XYWS_DEV cstate fallback_input(const st_params& P, uint64_t k, uint32_t lane) {
-  const uint64_t ts = k * SEG;
-  for (uint32_t it = 0; it < SPIN; it++) {
-    for (int64_t b = (int64_t)k - 1;; b -= 64) {
-      const int64_t j = b - (int64_t)lane;
-      const uint32_t fc = j >= 0 ? flag_load(P.fC + j) : (j == -1 ? 1u : 0u);
-      const uint64_t m = __ballot(fc >= 1);
-      if (!m) continue;  // none of these 64 published: look further back (j = -1 always is)
-      const int64_t jj = b - (int64_t)__builtin_ctzll(m);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      cstate S = jj >= 0 ? load_state(rec_of(P, (uint64_t)jj) + R_CO) : initial_state(P);
-      S.cnt = 0;
-      if (jj == (int64_t)k - 1 || (S.st & S_PARTIAL) || S.X >= ts) return S;
-      break;  // a nearer segment continues that chain: wait for it
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  atomicOr(P.head + 1, 32u);
-  cstate z = initial_state(P);
-  z.cnt = 0;
-  return z;
-}
-
-// Input state of segment k as the whole wave sees it (see the file comment).
-// kind: 0 exact, 1 speculated by link support, 2 fallback.
-XYWS_DEV cstate resolve_input(const st_params& P, st_lds& L, uint64_t k, uint32_t lane, uint32_t& kind) {
-  kind = 0;
-  cstate E0 = initial_state(P);
-  if (k == 0) return E0;
-  const uint64_t ts = k * SEG;
-  E0.cnt = 0;
-  if ((E0.st & S_PARTIAL) || E0.X >= ts) return E0;  // the batch start reaches k: exact
-  const int64_t w0 = (int64_t)k - (int64_t)(WIN - 1);
-  const int64_t g = w0 + (int64_t)lane;
-  // every window segment was ticketed before k and publishes its aggregate
-  // from local work only (long done, one index phase ago)
-  bool have = g < 0 || flag_load(P.fA + g) >= 1;
-  for (uint32_t it = 0; !__all(have) && it < SPIN; it++) {
-    __builtin_amdgcn_s_sleep(1);
-    if (!have) have = flag_load(P.fA + g) >= 1;
-  }
-  if (!__all(have)) atomicOr(P.head + 1, 64u);
-  have = have && g >= 0;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  stat_phase(P, ST_F_POLL, L.tstamp);
-  const uint64_t* r = rec_of(P, have ? (uint64_t)g : 0);
-  const uint32_t meta = have ? (uint32_t)st_load(r + R_META) : 0u;
-  uint64_t ent[NENT / 2], out[NOUT][2];
-#pragma unroll
-  for (uint32_t q = 0; q < NENT / 2; q++) ent[q] = have ? st_load(r + R_ENT0 + q) : 0;
-#pragma unroll
-  for (uint32_t o = 0; o < NOUT; o++) {
-    out[o][0] = have ? st_load(r + R_OUT0 + 2 * o) : 0;
-    out[o][1] = have ? st_load(r + R_OUT0 + 2 * o + 1) : 0;
-  }
-  const uint32_t ne = meta & 0xFF, no = (meta >> 8) & 0xFF;
-  L.bk_n[lane] = 0;
-  wave_sync();
-  // every outcome exit that lands inside a later window segment is a link candidate
-#pragma unroll
-  for (uint32_t o = 0; o < NOUT; o++) {
-    if (o < no) {
-      const uint64_t x = out[o][0];
-      if (x < P.hi) {
-        const int64_t u = (int64_t)(x / SEG) - w0;
-        if (u > (int64_t)lane && u < (int64_t)WIN) {
-          const uint32_t slot = atomicAdd(&L.bk_n[u], 1u);
-          if (slot < BKT) L.bk[u][slot] = (uint32_t)(x - (uint64_t)(w0 + u) * SEG);
-        }
-      }
-    }
-  }
-  if (lane == 0) {  // the batch start's exit supports too
-    const int64_t u = (int64_t)(E0.X / SEG) - w0;
-    if (E0.X < P.hi && u >= 0 && u < (int64_t)WIN) {
-      const uint32_t slot = atomicAdd(&L.bk_n[u], 1u);
-      if (slot < BKT) L.bk[u][slot] = (uint32_t)(E0.X - (uint64_t)(w0 + u) * SEG);
-    }
-  }
-  wave_sync();
-  stat_phase(P, ST_F_RECS, L.tstamp);
-  // each segment: the first entry that some exit lands on -> its outcome
-  const uint32_t nb = L.bk_n[lane] < BKT ? L.bk_n[lane] : BKT;
-  uint32_t oc = 0xFFu;
-#pragma unroll
-  for (uint32_t q = 0; q < NENT; q++) {
-    const uint32_t e = (uint32_t)(ent[q / 2] >> (32 * (q % 2)));
-    if (oc == 0xFFu && q < ne) {
-      for (uint32_t b = 0; b < nb; b++)
-        if (L.bk[lane][b] == (e & 0xFFFFu)) { oc = e >> 29; break; }
-    }
-  }
-  uint64_t dX = 0, dW = 0;
-#pragma unroll
-  for (uint32_t o = 0; o < NOUT; o++)
-    if (o == oc) { dX = out[o][0]; dW = out[o][1]; }
-  // k's input: the trusted outcome of the nearest earlier segment that reaches k
-  const uint64_t m = __ballot(oc != 0xFFu && lane < WIN - 1 && dX >= ts);
-  if (!m) {
-    kind = 2;
-    return fallback_input(P, k, lane);
-  }
-  kind = 1;
-  const uint32_t p = 63 - __builtin_clzll(m);
-  const uint64_t pss = (uint64_t)(w0 + (int64_t)p) * SEG;
-  const uint64_t w1 = rl64(dW, p);
-  cstate I;
-  I.cnt = 0;
-  I.X = rl64(dX, p);
-  I.cov_ps = pss + (w1 & 0xFFFFF);
-  I.cov_start = I.cov_ps - ((w1 >> 20) & 0xF);
-  I.cov_kw = (uint32_t)(w1 >> 32);
-  I.st = 0;
-  return I;
-}
-
-// Exclusive frame-count prefix of segment k (decoupled look-back sum).
-XYWS_DEV uint64_t count_prefix(const st_params& P, uint64_t k, uint32_t lane) {
-  uint32_t* err = P.head + 1;
-  uint64_t sum = 0;
-  int64_t b = (int64_t)k - 1;
-  for (uint32_t guard = 0; b >= 0 && guard < (1u << 20); guard++) {
-    const int64_t j = b - (int64_t)lane;
-    uint32_t fn = j >= 0 ? flag_load(P.fN + j) : 2u;
-    const uint64_t mi = __ballot(fn >= 2);
-    const uint32_t li = mi ? (uint32_t)__builtin_ctzll(mi) : 64u;
-    bool ready = lane >= li || fn >= 1;
-    for (uint32_t it = 0; !__all(ready) && it < SPIN; it++) {
-      __builtin_amdgcn_s_sleep(2);
-      if (!ready) { fn = flag_load(P.fN + j); ready = fn >= 1; }
-    }
-    if (!__all(ready)) { atomicOr(err, 8u); return sum; }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint64_t v = 0;
-    if (lane < li) v = st_load(rec_of(P, (uint64_t)j) + R_NA);
-    else if (lane == li && j >= 0) v = st_load(rec_of(P, (uint64_t)j) + R_NI);
-#pragma unroll
-    for (uint32_t o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);  // lanes > li hold 0
-    sum += v;
-    if (mi) break;
-    b -= 64;
-  }
-  return sum;
-}
-
-// The frames of segment k from input s (lane 0): the path from the entry
-// survivor through the jump tables (mode 1), or an exact header chase (mode 2).
-struct chain_res {
-  cstate o;
-  uint32_t mode, node, rem;
 };
 
-XYWS_DEV chain_res own_chain(const st_params& P, const sv_buf& S, uint32_t nsurv, uint64_t ss,
-                             uint64_t se, const cstate& s) {
-  chain_res c;
-  c.o = s; c.mode = 0; c.node = 0; c.rem = 0;
-  if ((s.st & S_PARTIAL) || s.X >= se || s.X >= P.hi) return c;
-  const uint32_t xr = (uint32_t)(s.X - ss);
-  uint32_t x = 0, y = nsurv;
-  while (x < y) {
-    const uint32_t m = (x + y) >> 1;
-    if (S.pos[m] < xr) x = m + 1; else y = m;
-  }
-  if (x < nsurv && S.pos[x] == xr && S.out[x] < NOUT) {
-    const uint32_t oc = S.out[x];
-    c.mode = 1;
-    c.node = x;
-    c.rem = S.rem[x];
-    c.o.X = S.outs[oc][0]; c.o.cov_ps = S.outs[oc][1]; c.o.cov_start = S.outs[oc][2];
-    c.o.cov_kw = (uint32_t)S.outs[oc][3];
-    c.o.cnt = s.cnt + c.rem;
-    c.o.st = 0;
-  } else {
-    c.mode = 2;  // the caller chases (chase_global) once seg+1's first bytes are published
-  }
-  return c;
+// ---------------------------------------------------------------- the chase
+// XOR words for the 16-byte chunk at segment offset a; entries are contiguous
+// frames sorted by start, g = the last entry starting at or before a.
+// Byte-select mask of the bytes of the word at segment offset a (a % 4 == 0)
+// that lie in [lo, hi).
+XYWS_DEV uint32_t range_mask32(uint32_t a, uint32_t lo, uint32_t hi) {
+  if (hi <= a || lo >= a + 4) return 0u;
+  const uint32_t l = lo > a ? lo - a : 0u;
+  const uint32_t h = hi - a < 4u ? hi - a : 4u;
+  const uint32_t mh = h >= 4 ? 0xFFFFFFFFu : ((1u << (8u * h)) - 1u);
+  return mh & ~((1u << (8u * l)) - 1u);
 }
 
-XYWS_DEV void write_frame(const st_params& P, uint64_t ord, uint64_t start, const hdr_info& h,
-                          uint64_t ps, int32_t hdr_shift) {
-  if (!P.frames || ord >= P.cap) return;
-  xyws_frame f;
-  f.frame_off = (int64_t)(start - P.lo) - hdr_shift;
-  f.payload_off = (int64_t)(ps - P.lo);
-  f.payload_len = h.plen;
-  f.key[0] = (uint8_t)h.key; f.key[1] = (uint8_t)(h.key >> 8);
-  f.key[2] = (uint8_t)(h.key >> 16); f.key[3] = (uint8_t)(h.key >> 24);
-  f.flags = h.flags;
-  f.hdr_len = (uint8_t)h.hlen;
-  f.status = (uint8_t)(h.status | (sat_add(ps, h.plen) > P.hi ? XYWS_ST_PAYLOAD_INCOMPLETE : 0));
-  f.reserved = 0;
-  P.frames[ord] = f;
-}
-
-// XOR words for the 16-byte chunk at segment offset a. Entries are contiguous
-// frames sorted by start; g = the last entry starting at or before a. Common
-// case: one frame's payload covers the whole chunk.
-XYWS_DEV u32x4 chunk_xor(const st_lds& L, uint32_t nfl, uint32_t g, uint32_t a) {
-  const fent e = L.flist[g];
-  if (e.ps <= a && e.end >= a + 16) return u32x4{e.kw, e.kw, e.kw, e.kw};
+template <class G>
+XYWS_DEV u32x4 chunk_xor(const lds_t<G>& L, uint32_t nfl, uint32_t g, uint32_t a) {
   u32x4 w = {0u, 0u, 0u, 0u};
   for (uint32_t h = g; h < nfl; h++) {
-    const fent f = L.flist[h];
+    const fent f = L.fl[h];
     if (h != g && f.start >= a + 16) break;
-    w.x |= f.kw & range_mask(a, f.ps, f.end);
-    w.y |= f.kw & range_mask(a + 4, f.ps, f.end);
-    w.z |= f.kw & range_mask(a + 8, f.ps, f.end);
-    w.w |= f.kw & range_mask(a + 12, f.ps, f.end);
+    w.x |= f.kw & range_mask32(a, f.ps, f.end);
+    w.y |= f.kw & range_mask32(a + 4, f.ps, f.end);
+    w.z |= f.kw & range_mask32(a + 8, f.ps, f.end);
+    w.w |= f.kw & range_mask32(a + 12, f.ps, f.end);
   }
   return w;
 }
 
-XYWS_DEV __amdgpu_buffer_rsrc_t seg_rsrc(const st_params& P, uint64_t ss) {
-  // [ss, ss + round16(hi - ss)) capped at SEG + 16: chunks past the batch read as zero
-  const uint64_t room = P.hi - ss;
-  const uint32_t nrec = room >= SEG + 16 ? SEG + 16 : (uint32_t)((room + 15) & ~15ull);
-  return __builtin_amdgcn_make_buffer_rsrc(P.base + ss, 0, nrec, 0x00020000);
+// One pass of the chase over segment [ss, ss+SEG), lane 0: the frame covering
+// the pass start, then frames parsed from X, up to FCAP entries. Sets
+// pass_hi: the chunks below it are final for this pass.
+template <class G>
+XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t lo_c) {
+  const uint64_t se = ss + G::SEG;
+  cstate S = L.S;
+  uint32_t n = 0;
+  if (!(S.st & (S_NOCOV | S_PARTCARRY)) && S.X > ss + lo_c) {
+    fent e;
+    e.start = 0;
+    e.ps = clamp_rel(S.cov_ps, ss);
+    e.end = clamp_rel(S.X, ss);
+    e.kw = S.cov_kw;
+    L.fl[n++] = e;
+  }
+  const bool known = L.known != 0;
+  const uint64_t lim = known ? L.Wn : NONE, hn = L.hn;
+  bool past = L.past != 0, done = false, end = false;
+  uint64_t cnt = 0, tail = 0;
+  for (;;) {
+    const uint64_t X = S.X;
+    if (known && !past && X >= hn) {  // the chain reached the successor's entry
+      past = true;
+      L.first_after = X;
+      L.ok = X == hn;
+    }
+    if (X >= P.hi || (S.st & (S_PARTIAL | S_CUT))) { end = true; break; }
+    if (X >= lim) { done = true; break; }
+    if (X >= se || n >= FCAP) break;
+    const hdr_info h = hdr_at(P, L, ss, X, lim);
+    if (!h.hlen) {
+      // incomplete: at the batch end (carry) or at the successor's write start
+      const bool at_end = lim >= P.hi || X + XYWS_MAX_FRAME_HEADER_SIZE <= lim;
+      S.st = (S.st & (S_NOCOV | S_CARRIED | S_HDRCARRY)) | (at_end ? S_PARTIAL : S_CUT);
+      end = true;
+      if (!at_end) { done = true; stat_add(P, ST_CUT, 1); }
+      break;
+    }
+    const cstate F = frame_state(X, h);
+    fent e;
+    e.start = clamp_rel(X, ss);
+    e.ps = clamp_rel(F.cov_ps, ss);
+    e.end = clamp_rel(F.X, ss);
+    e.kw = F.cov_kw;
+    L.fl[n++] = e;
+    if (past) tail++; else cnt++;
+    S = F;
+  }
+  L.past = past;
+  if (done) L.done = 1;
+  if (end) L.end = 1;
+  L.cnt += cnt;
+  L.tail += tail;
+  L.S = S;
+  L.nfl = n;
+  const bool seg_done = S.X >= se || end || done;
+  L.pass_hi = seg_done ? G::SEG : (uint32_t)((S.X - ss) & ~15ull);
 }
 
-// ---------------------------------------------------------------- unmask application
-// Frames of segment `seg` from input `sin` (whole workgroup): the covering
-// frame, then the path (mode 1, from survivor `node`, `rem` frames) or an exact
-// chase (mode 2) in passes of FCAP entries; XOR words accumulate in registers;
-// then the changed chunks are loaded, XORed and stored. Descriptors from
-// ordinal fb when `emit`.
-XYWS_DEV void apply_frames(const st_params& P, st_lds& L, const sv_buf* S, uint64_t seg,
-                           const cstate& sin, uint32_t mode, uint32_t node, uint32_t rem, uint64_t fb,
-                           bool emit, uint32_t tid, bool stamp = false) {
-  const uint64_t ss = seg * SEG, se = ss + SEG, hi = P.hi;
-  const bool parse_only = (P.opts & XYWS_OPT_PARSE_ONLY) != 0;
-  emit = emit && P.frames;
-  __syncthreads();  // the frame list overlays the index stage's sub-tile
-  if (tid == 0) {
-    L.nfl = 0;
-    if (!(sin.st & (S_NOCOV | S_PARTCARRY))) {  // covering entry: frame begun before ss
-      fent e;
-      e.start = 0;
-      e.ps = clamp_rel(sin.cov_ps, ss);
-      e.end = clamp_rel(sin.X, ss);
-      e.kw = sin.cov_kw;
-      L.flist[0] = e;
-      L.nfl = 1;
+// The next run after `run` that has an entry (lane 0). Waits for each
+// candidate's prologue; every one of them took its ticket after ours.
+XYWS_DEV void lookup_successor(const run_params& P, uint64_t& hn, uint64_t& Wn, uint64_t& succ, uint32_t run) {
+  for (uint32_t j = run + 1; j < P.nruns; j++) {
+    uint32_t it = 0;
+    while (flag_load(P.flags + j) == 0u && it < SPIN) {
+      __builtin_amdgcn_s_sleep(2);
+      it++;
     }
-    L.fbase = fb;
-    L.chase_X = sin.X;
-    L.pass_done = (mode != 2);
+    if (it) stat_add(P, ST_SPIN, it);
+    if (it >= SPIN) atomicOr(P.head + 1, 2u);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t h = st_load(P.rec + (uint64_t)j * R_WORDS + R_H);
+    if (h != NONE) {
+      hn = h;
+      Wn = st_load(P.rec + (uint64_t)j * R_WORDS + R_W);
+      succ = j;
+      return;
+    }
   }
-  __syncthreads();
-  if (mode == 1) {
-    // frame d of the path from node x is its d-th successor: binary lifting
-    const uint32_t base_n = L.nfl;
-    for (uint32_t dd = tid; dd < rem; dd += NT) {
-      uint32_t i = node;
+  hn = NONE;
+  Wn = NONE;
+  succ = P.nruns;
+}
+
+// Apply the chain in L.S (set by lane 0 together with L.known/hn/Wn/succ and
+// zeroed counters) from segment s0: every byte in [wlo, write limit) is XORed
+// with the key of the frame covering it, the write limit being the successor's
+// W (looked up before the first segment at or past rng_end, unless known). The
+// chase stops at the successor's W; L.ok tells whether it landed on its entry.
+template <class G>
+XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint64_t s0,
+                        bool in_lds, uint64_t wlo, uint64_t rng_end, uint32_t run) {
+  const bool stores = (P.opts & XYWS_OPT_PARSE_ONLY) == 0;
+  const uint64_t wl = wlo > P.lo ? wlo : P.lo;
+  // Pipeline: the registers of `io` always hold the loads of the segment the
+  // next iteration fills into LDS, issued one iteration ahead; every pass
+  // issues exactly CH stores per lane (skipped chunks go to an out-of-range
+  // offset), so each fill waits for its loads only (vmcnt counts loads and
+  // stores together, in issue order) while the previous segment's stores drain.
+  if (!in_lds && io.pf != s0) io.issue(P, s0, tid);
+  {
+    // CH dropped stores (out-of-range offset: no memory traffic) so that on
+    // every path into the loop at least CH stores are younger than the loads:
+    // the compiler's wait before the fill is then vmcnt(CH), not vmcnt(0)
+    const __amdgpu_buffer_rsrc_t rz = seg_rsrc<G>(P, s0);
 #pragma unroll
-      for (uint32_t bb = 0; bb < LV; bb++)
-        if ((dd >> bb) & 1u) i = S->jmp[bb][i];
-      const uint64_t p = ss + S->pos[i];
-      const uint64_t ps = p + S->hlen[i];
-      fent e;
-      e.start = S->pos[i];
-      e.ps = (uint32_t)(ps - ss);
-      e.end = S->nrel[i];
-      e.kw = aligned_key(S->key[i], ps, 0);
-      L.flist[base_n + dd] = e;
-      if (emit) write_frame(P, fb + dd, p, header_safe(P, p), ps, 0);
+    for (uint32_t k = 0; k < G::CH; k++)
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rz, OOB, 0, AUX_NT);
+  }
+  // stats builds: wave 0 accumulates phase cycles in registers, flushed once
+  const bool st_on = stats_on(P) && tid < 64;
+  uint64_t tm = st_on ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t acc_tail = 0, acc_fill = 0, acc_pf = 0, acc_cp = 0, acc_sync = 0, acc_xor = 0;
+#define XYWS_STAMP(acc)                                 \
+  do {                                                  \
+    if (st_on) {                                        \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+      acc += t_ - tm;                                   \
+      tm = t_;                                          \
+    }                                                   \
+  } while (0)
+  for (uint64_t s = s0;; s++) {
+    const uint64_t ss = s * G::SEG, nx = ss + G::SEG;
+    __syncthreads();  // the previous segment's LDS reads are done
+    XYWS_STAMP(acc_tail);
+    if (tid == 0 && !L.known && nx >= rng_end) {
+      // the next segment lies past the run's range: the write limit is the
+      // successor's W (its prologue published it long ago)
+      const uint64_t t0 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
+      uint64_t hn, Wn, succ;
+      lookup_successor(P, hn, Wn, succ, run);
+      L.hn = hn; L.Wn = Wn; L.succ = succ; L.known = 1;
+      if (stats_on(P)) stat_add(P, ST_T_WAIT, __builtin_amdgcn_s_memtime() - t0);
+    }
+    if (!(in_lds && s == s0)) {
+#pragma unroll
+      for (uint32_t k = 0; k < G::CH; k++)
+        *reinterpret_cast<u32x4*>(&L.seg[(k * G::NT + tid) * 16u]) = io.e[k];
+      io.pf = NONE;
     }
     __syncthreads();
-    if (tid == 0) L.nfl = base_n + rem;
-  }
-  // Passes of at most FCAP entries. Pass p applies the chunks in [lo_c, hi_c):
-  // hi_c = the chunk-aligned start of its last frame (SEG for the final pass);
-  // the frames reaching past hi_c carry into the next pass. Every chunk is
-  // loaded, XORed and stored once, its loads issued before its XOR words are
-  // built.
-  const __amdgpu_buffer_rsrc_t rs = seg_rsrc(P, ss);
-  const uint32_t voff = tid * 16u;
-  const uint64_t lim64 = hi - ss;
-  const uint32_t lim = lim64 < SEG ? (uint32_t)lim64 : SEG;  // bytes of this segment in the batch
-  uint32_t lo_c = 0;
-  for (;;) {
-    if (mode == 2 && tid == 0) {  // exact chase, up to FCAP entries per pass
-      uint64_t X = L.chase_X, ord = L.fbase;
-      uint32_t n = L.nfl;
-      const uint64_t stop = se < hi ? se : hi;
-      while (X < stop && n < FCAP) {
-        hdr_info hh = header_safe(P, X);
-        if (!hh.hlen) { X = ~0ull; break; }
-        const uint64_t ps = X + hh.hlen;
-        fent e;
-        e.start = (uint32_t)(X - ss);
-        e.ps = (uint32_t)(ps - ss);
-        e.end = clamp_rel(sat_add(ps, hh.plen), ss);
-        e.kw = aligned_key(hh.key, ps, 0);
-        L.flist[n++] = e;
-        if (emit) write_frame(P, ord, X, hh, ps, 0);
-        ord++;
-        X = sat_add(ps, hh.plen);
-      }
-      L.nfl = n;
-      L.fbase = ord;
-      L.chase_X = X;
-      L.pass_done = !(X < stop);
-    }
-    __syncthreads();
-    const uint32_t nfl = L.nfl;
-    const uint32_t done = L.pass_done;
-    const uint32_t hi_c = (done || !nfl) ? SEG : (L.flist[nfl - 1].start & ~15u);
-    if (!parse_only && nfl) {
-      u32x4 d[CHS];
-#pragma unroll
-      for (uint32_t k = 0; k < CHS; k++) {
-        const uint32_t a = (k * NT + tid) * 16u;
-        d[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (a >= lo_c && a < hi_c) ? voff : OOB, k * NT * 16u, 0);
-      }
+    XYWS_STAMP(acc_fill);
+    const bool known = L.known != 0;
+    const uint64_t wlim = known ? L.Wn : rng_end;
+    const uint64_t whi = wlim < P.hi ? wlim : P.hi;
+    const bool fin0 = (L.end || L.done) && nx >= whi;
+    if (nx < P.hi && nx < wlim && !fin0 && io.pf != s + 1) io.issue(P, s + 1, tid);
+    XYWS_STAMP(acc_pf);
+    const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, s);
+    uint32_t lo_c = 0;
+    for (;;) {
+      if (tid == 0) chase_pass(P, L, ss, lo_c);
+      XYWS_STAMP(acc_cp);
+      __syncthreads();
+      XYWS_STAMP(acc_sync);
+      const uint32_t nfl = L.nfl, hi_c = L.pass_hi;
+      // each lane walks the sorted, contiguous frame list once, forward with
+      // its chunks: entry g covers the chunk when no later entry starts in it
+      // and its payload spans it (the common case: one key word for all four
+      // dwords); chunks holding a header or a frame boundary take chunk_xor
+      // write window [wl, whi) relative to the segment (32-bit compares below)
+      const uint32_t wl_r = wl > ss ? (wl - ss < G::SEG ? (uint32_t)(wl - ss) : G::SEG) : 0u;
+      const uint32_t wh_r = whi > ss ? (whi - ss < G::SEG ? (uint32_t)(whi - ss) : G::SEG) : 0u;
+      const bool any = stores && nfl && wl_r < wh_r;
       uint32_t g = 0, edge = 0;
+      fent e = L.fl[0];
+      uint32_t ns = nfl > 1 ? L.fl[1].start : 0xFFFFFFFFu;
 #pragma unroll
-      for (uint32_t k = 0; k < CHS; k++) {
-        const uint32_t a = (k * NT + tid) * 16u;  // increases with k: g only moves forward
-        while (g + 1 < nfl && L.flist[g + 1].start <= a) g++;
-        const u32x4 x = chunk_xor(L, nfl, g, a);
-        const bool nz = (x.x | x.y | x.z | x.w) != 0u;
-        const bool inr = a >= lo_c && a < hi_c;
-        const bool inb = a + 16 <= lim && !(ss == 0 && a < P.lo);
-        __builtin_amdgcn_raw_buffer_store_b128(d[k] ^ x, rs, (inr && nz && inb) ? voff : OOB, k * NT * 16u, 0);
-        if (inr && nz && !inb) edge |= 1u << k;
+      for (uint32_t k = 0; k < G::CH; k++) {
+        const uint32_t a = (k * G::NT + tid) * 16u;
+        const bool in = any && a >= lo_c && a < hi_c && a + 16 > wl_r && a < wh_r;
+        u32x4 m = {0u, 0u, 0u, 0u};
+        if (in) {
+          while (ns <= a) {
+            g++;
+            e = L.fl[g];
+            ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
+          }
+          if (e.ps <= a && e.end >= a + 16 && ns >= a + 16) m = u32x4{e.kw, e.kw, e.kw, e.kw};
+          else m = chunk_xor(L, nfl, g, a);
+        }
+        const bool nz = (m.x | m.y | m.z | m.w) != 0u;
+        const bool full = a >= wl_r && a + 16 <= wh_r;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
+        __builtin_amdgcn_raw_buffer_store_b128(v ^ m, rs,
+                                               (in && nz && full && !(P.opts & XYWS_OPT_NO_STORE)) ? tid * 16u : OOB,
+                                               k * G::NT * 16u, AUX_NT);
+        // hipcc (ROCm 7.2, gfx950) may overwrite a dwordx4 store's data VGPRs
+        // in the very next instruction; later lanes then store the new value
+        // (seen as wrong bytes in dword 0, lanes 12-15 of each 16). Two wait
+        // states after the store; inline asm is a scheduling boundary.
+        asm volatile("s_nop 1" ::: "memory");
+        if (in && nz && !full) edge |= 1u << k;
       }
-      // first/last chunk of the batch: only the caller's bytes (rare, not unrolled)
 #pragma nounroll
-      while (edge) {
+      while (edge) {  // the batch's first/last chunk: only the bytes in [wl, whi)
         const uint32_t k = __builtin_ctz(edge);
         edge &= edge - 1;
-        const uint32_t a = (k * NT + tid) * 16u;
-        uint32_t ge = 0;
-        while (ge + 1 < nfl && L.flist[ge + 1].start <= a) ge++;
-        const u32x4 x = chunk_xor(L, nfl, ge, a);
-        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+        const uint32_t a = (k * G::NT + tid) * 16u;
+        const uint64_t A = ss + a;
+        uint32_t x = 0, y = nfl;
+        while (y - x > 1) {
+          const uint32_t mid = (x + y) >> 1;
+          if (L.fl[mid].start <= a) x = mid; else y = mid;
+        }
+        const u32x4 m = chunk_xor(L, nfl, x, a);
 #pragma nounroll
         for (uint32_t t = 0; t < 16; t++) {
-          const uint64_t q = ss + a + t;
-          const uint8_t kb = (uint8_t)(w[t >> 2] >> (8u * (t & 3u)));
-          if (kb && q >= P.lo && q < hi) P.base[q] ^= kb;
+          const uint64_t q = A + t;
+          const uint32_t mw = t < 4 ? m.x : t < 8 ? m.y : t < 12 ? m.z : m.w;
+          const uint8_t kb = (uint8_t)(mw >> (8u * (t & 3u)));
+          if (kb && q >= wl && q < whi) P.base[q] = L.seg[a + t] ^ kb;
         }
       }
+      XYWS_STAMP(acc_xor);
+      if (hi_c >= G::SEG) break;
+      __syncthreads();  // the list is rebuilt for the next pass
+      lo_c = hi_c;
     }
-    if (stamp && tid < 64 && done) stat_phase(P, ST_F_ACCUM, L.tstamp);
-    __syncthreads();
-    if (done) break;
-    if (tid == 0) {  // carry the frames reaching past hi_c into the next pass
-      uint32_t c = nfl;
-      while (c > 0 && L.flist[c - 1].end > hi_c) c--;
-      for (uint32_t i = c; i < nfl; i++) L.flist[i - c] = L.flist[i];
-      L.nfl = nfl - c;
-    }
-    lo_c = hi_c;
-    __syncthreads();
+    // continue while bytes below the write limit remain
+    const bool fin = (L.end || L.done) && nx >= whi;
+    if (nx >= P.hi || nx >= wlim || fin) break;
   }
+  if (st_on && tid == 0) {
+    stat_add(P, ST_T_TAIL, acc_tail);
+    stat_add(P, ST_T_FILL, acc_fill);
+    stat_add(P, ST_T_PF, acc_pf);
+    stat_add(P, ST_T_CP, acc_cp);
+    stat_add(P, ST_T_CHASE, acc_sync);
+    stat_add(P, ST_T_XOR, acc_xor);
+  }
+#undef XYWS_STAMP
+  __syncthreads();
 }
 
-// ---------------------------------------------------------------- index stage
-XYWS_DEV void index_segment(const st_params& P, st_lds& L, uint64_t seg, uint32_t tid, uint32_t lane,
-                            uint32_t wave) {
-  sv_buf& S = L.sv;
-  const bool want_unmasked = (P.opts & XYWS_OPT_UNMASKED_HINT) != 0;
-  const uint64_t lo = P.lo, hi = P.hi;
-  const uint64_t ss = seg * SEG;
-  uint64_t* rec = P.recs + seg * R_WORDS;
-
-  // ---- 1. loads: the whole segment into registers
-  const __amdgpu_buffer_rsrc_t rs = seg_rsrc(P, ss);
-  const uint32_t voff = tid * 16u;
-  u32x4 d[CHS];
-#pragma unroll
-  for (uint32_t k = 0; k < CHS; k++) d[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, k * NT * 16u, 0);
-  u32x4 halo = {0u, 0u, 0u, 0u};
-  if (tid == 0) halo = __builtin_amdgcn_raw_buffer_load_b128(rs, 0, SEG, 0);
-  if (tid == 0) { S.nsurv = 0; S.overflow = 0; S.seg = seg; }
-  if (wave == 0) stat_phase(P, ST_F_ISSUE, L.tstamp);
-  if (tid < 2) {  // the segment's first 32 bytes, for headers straddling into it
-    st_store(rec + R_HEAD + 2 * tid, (uint64_t)d[0].x | ((uint64_t)d[0].y << 32));
-    st_store(rec + R_HEAD + 2 * tid + 1, (uint64_t)d[0].z | ((uint64_t)d[0].w << 32));
-  }
-  if (wave == 0) stat_phase(P, ST_F_HEAD, L.tstamp);
-
-  // ---- 1b. per sub-tile: LDS copy, prefilter, candidates -> survivors
-#pragma nounroll
-  for (uint32_t s = 0; s < NSUB; s++) {
-    const uint64_t ts = ss + (uint64_t)s * SUB, te = ts + SUB;
-    __syncthreads();  // previous sub-tile (or the previous unmask stage's list) consumed
-    // sub-tile s is always d[0 .. CHSUB): the chunk registers shift down by
-    // CHSUB after each sub-tile (register moves, no dynamic indexing)
-#pragma unroll
-    for (uint32_t k = 0; k < CHSUB; k++) *reinterpret_cast<u32x4*>(&L.sub[(k * NT + tid) * 16u]) = d[k];
-    if (tid == 0) *reinterpret_cast<u32x4*>(&L.sub[SUB]) = s + 1 < NSUB ? d[CHSUB] : halo;
-#pragma unroll
-    for (uint32_t k = 0; k + CHSUB < CHS; k++) d[k] = d[k + CHSUB];
-    __syncthreads();
-    if (s == 0 && wave == 0) stat_phase(P, ST_F_STAGE0, L.tstamp);
-    // prefilter: lane owns sub-tile positions [tid*32, tid*32+32)
-    const uint32_t p0 = tid * PPL;
-    uint32_t cand = 0;
-    {
-      uint32_t w = *reinterpret_cast<const uint32_t*>(&L.sub[p0]);
-#pragma unroll
-      for (uint32_t i = 0; i < PPL / 4; i++) {
-        const uint32_t wn = *reinterpret_cast<const uint32_t*>(&L.sub[p0 + 4 * i + 4]);
-        const uint32_t b1s = (w >> 8) | (wn << 24);  // byte t = byte at position 4i+t+1
-        const uint32_t rsv_ok = ~((w & 0x70707070u) + 0x70707070u) & 0x80808080u;
-        const uint32_t bad_op = ((w << 5) | ((w & (w >> 1)) << 7)) & 0x80808080u;
-        const uint32_t m_ok = (want_unmasked ? ~b1s : b1s) & 0x80808080u;
-        const uint32_t c = rsv_ok & ~bad_op & m_ok;
-        const uint32_t nib = ((c >> 7) | (c >> 14) | (c >> 21) | (c >> 28)) & 0xFu;
-        cand |= nib << (4 * i);
-        w = wn;
-      }
-      const uint64_t st = ts + p0;
-      uint32_t m = ~0u;
-      if (st + PPL > hi) m = (st >= hi) ? 0 : ((1u << (hi - st)) - 1);
-      if (st < lo) m &= (lo - st >= PPL) ? 0 : ~((1u << (lo - st)) - 1);
-      cand &= m;
-      L.bits[tid] = cand;
+// ---------------------------------------------------------------- prologue
+// Earliest position of run `run`'s range whose chain of KHDR headers is
+// plausible (lane 0 returns it through L.aux0; NONE if there is none). Leaves
+// the segment it was found in (L.aux1) in LDS.
+template <class G>
+XYWS_DEV bool chain_plausible(const run_params& P, const lds_t<G>& L, uint64_t ss, uint64_t q, bool unm) {
+  uint64_t x = q;
+  uint32_t need = KHDR_7;
+  for (uint32_t i = 0; i < need; i++) {
+    if (x >= P.hi) return i > 0;  // the chain ends with the batch
+    const hdr_info h = hdr_at(P, L, ss, x, NONE);
+    if (!h.hlen) return i > 0;    // a header cut by the batch end
+    if (!plausible(h, unm)) return false;
+    if (i == 0) {
+      const uint32_t ext = h.hlen - 2 - ((h.status & XYWS_ST_UNMASKED) ? 0u : 4u);
+      need = ext == 8 ? KHDR_127 : ext == 2 ? KHDR_126 : KHDR_7;
     }
+    x = sat_add(x + h.hlen, h.plen);
+  }
+  return true;
+}
+
+template <class G>
+XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint32_t run) {
+  const bool unm = (P.opts & XYWS_OPT_UNMASKED_HINT) != 0;
+  const uint64_t s_begin = (uint64_t)run * P.spr;
+  uint64_t s_end = s_begin + P.spr;
+  if (s_end > P.nseg) s_end = P.nseg;
+  if (tid == 0) L.aux0 = NONE;
+  for (uint64_t s = s_begin; s < s_end; s++) {
+    const uint64_t ss = s * G::SEG;
     __syncthreads();
-    // candidates: the successor must be a candidate too (or lie past the sub-tile)
-    uint32_t surv = 0;
-    {
-      uint32_t m = cand;
-      while (m) {
-        const uint32_t b = __builtin_ctz(m);
-        m &= m - 1;
-        const uint32_t prel = p0 + b;
-        const uint64_t pabs = ts + prel;
-        const uint32_t b0 = L.sub[prel], b1 = L.sub[prel + 1];
-        const uint32_t l7 = b1 & 0x7Fu;
-        uint64_t nx;
-        if (l7 < 126) {  // short form: no further bytes needed
-          if ((b0 & 0x08u) && !(b0 & 0x80u)) continue;  // control frame without FIN
-          nx = pabs + 2 + 4 * (b1 >> 7) + l7;
-        } else {
-          hdr_info hh = header_lds(L.sub, prel, pabs, hi);
-          if (!plausible(hh, (uint8_t)b1)) continue;
-          nx = sat_add(pabs + hh.hlen, hh.plen);
+    io.fill(P, L, s, tid);
+    if (tid == 0) { L.best = 0xFFFFFFFFu; L.aux1 = s; }
+    __syncthreads();
+    if (s + 1 < P.nseg) io.issue(P, s + 1, tid);
+    bool found = false;
+#pragma unroll 1
+    for (uint32_t k = 0; k < G::CH && !found; k++) {
+      const uint32_t a = (k * G::NT + tid) * 16u;
+      const uint64_t A = ss + a;
+      if (A >= P.hi) break;
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(L.seg + a);
+      const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+      uint32_t bits = cand_nibble(w0, w1, unm) | (cand_nibble(w1, w2, unm) << 4) |
+                      (cand_nibble(w2, w3, unm) << 8) | (cand_nibble(w3, w4, unm) << 12);
+      // headers straddling the segment end are left to the next segment's scan
+      if (a + 16 + 1 > G::SEG) bits &= (1u << (G::SEG - XYWS_MAX_FRAME_HEADER_SIZE - a + 1)) - 1u;
+      while (bits) {
+        const uint32_t t = __builtin_ctz(bits);
+        bits &= bits - 1;
+        const uint32_t pos = a + t;
+        if (pos > __hip_atomic_load(&L.best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+          found = true;
+          break;
         }
-        if (nx > hi) continue;
-        if (nx < te) {
-          const uint32_t nr = (uint32_t)(nx - ts);
-          if (!((L.bits[nr >> 5] >> (nr & 31)) & 1u)) continue;
-        }
-        surv |= 1u << b;
-      }
-    }
-    // ordered append: block-exclusive scan of per-lane survivor counts
-    uint32_t tot;
-    const uint32_t r0 = block_scan(L, __popc(surv), lane, wave, tot);
-    const uint32_t base_n = S.nsurv;
-    const bool fits = base_n + tot <= SMAX;
-    if (fits) {
-      uint32_t r = base_n + r0;
-      uint32_t m = surv;
-      while (m) {
-        const uint32_t b = __builtin_ctz(m);
-        m &= m - 1;
-        const uint32_t prel = p0 + b;
-        hdr_info hh = header_lds(L.sub, prel, ts + prel, hi);
-        S.pos[r] = s * SUB + prel;
-        S.nrel[r] = clamp_rel(sat_add(ts + prel + hh.hlen, hh.plen), ss);
-        S.key[r] = hh.key;
-        S.hlen[r] = (uint8_t)hh.hlen;
-        r++;
-      }
-    }
-    __syncthreads();
-    if (tid == 0) {
-      if (fits) S.nsurv = base_n + tot;
-      else S.overflow = 1;
-    }
-  }
-  __syncthreads();
-  if (wave == 0) stat_phase(P, ST_T_INDEX, L.tstamp);
-
-  // ---- 2. link survivors
-  const uint32_t nsurv = S.overflow ? 0u : S.nsurv;
-  for (uint32_t i = tid; i < nsurv; i += NT) {
-    const uint32_t nr = S.nrel[i];
-    uint16_t nn = N_EXIT;
-    if (nr < SEG) {
-      uint32_t x = i + 1, y = nsurv;  // successor lies after i: search (i, nsurv)
-      while (x < y) {
-        const uint32_t m = (x + y) >> 1;
-        if (S.pos[m] < nr) x = m + 1; else y = m;
-      }
-      nn = (x < nsurv && S.pos[x] == nr) ? (uint16_t)x : N_DEAD;
-    }
-    L.nxt[i] = nn;
-    S.jmp[0][i] = (nn == N_EXIT || nn == N_DEAD) ? J_TERM : nn;
-    S.rem[i] = 1;
-    L.last[i] = nn == N_EXIT ? (uint16_t)i : (nn == N_DEAD ? T_DEAD : 0);
-  }
-  __syncthreads();
-
-  // ---- 2a. pointer doubling: after round b, rem/last are final for chains of
-  // up to 2^(b+1) nodes and jmp[b+1] holds the 2^(b+1)-th successors
-  for (uint32_t b = 0; b < LV; b++) {
-    uint32_t nj[NPT], nr[NPT], nl[NPT];
-    bool any = false;
-#pragma unroll
-    for (uint32_t h = 0; h < NPT; h++) {
-      const uint32_t i = tid + h * NT;
-      nj[h] = J_TERM; nr[h] = 0; nl[h] = 0;
-      if (i < nsurv) {
-        const uint32_t j = S.jmp[b][i];
-        nr[h] = S.rem[i];
-        nl[h] = L.last[i];
-        if (j != J_TERM) {
-          const uint32_t jj = b + 1 < LV ? S.jmp[b][j] : J_TERM;
-          nj[h] = jj;
-          nr[h] += S.rem[j];
-          nl[h] = L.last[j];
-          any = any || jj != J_TERM;
+        if (chain_plausible(P, L, ss, ss + pos, unm)) {
+          atomicMin(&L.best, pos);
+          found = true;
+          break;
         }
       }
     }
     __syncthreads();
-#pragma unroll
-    for (uint32_t h = 0; h < NPT; h++) {
-      const uint32_t i = tid + h * NT;
-      if (i < nsurv) {
-        if (b + 1 < LV) S.jmp[b + 1][i] = (uint16_t)nj[h];
-        S.rem[i] = (uint16_t)nr[h];
-        L.last[i] = (uint16_t)nl[h];
-      }
-    }
-    const bool more = __syncthreads_or(any);
-    if (!more) {  // every chain resolved: the remaining levels are all J_TERM
-      for (uint32_t bb = b + 2; bb < LV; bb++)
-        for (uint32_t i = tid; i < nsurv; i += NT) S.jmp[bb][i] = J_TERM;
+    if (L.best != 0xFFFFFFFFu) {
+      if (tid == 0) L.aux0 = ss + L.best;
       break;
     }
   }
-  // outcome ids: chain-end nodes ranked in position order (thread tid owns
-  // nodes NPT*tid .. NPT*tid+NPT-1)
-  {
-    uint32_t isl[NPT], nl = 0;
-#pragma unroll
-    for (uint32_t h = 0; h < NPT; h++) {
-      const uint32_t i = NPT * tid + h;
-      isl[h] = (i < nsurv && L.nxt[i] == N_EXIT) ? 1u : 0u;
-      nl += isl[h];
-    }
-    uint32_t tot;
-    uint32_t id = block_scan(L, nl, lane, wave, tot);
-#pragma unroll
-    for (uint32_t h = 0; h < NPT; h++) {
-      const uint32_t i = NPT * tid + h;
-      if (isl[h]) {
-        S.out[i] = id < NOUT ? (uint8_t)id : O_UNREC;
-        if (id < NOUT) {
-          const uint64_t pp = ss + S.pos[i];
-          const uint64_t ps = pp + S.hlen[i];
-          S.outs[id][0] = S.nrel[i] == 0xFFFFFFFFu ? ~0ull : ss + S.nrel[i];
-          S.outs[id][1] = ps;
-          S.outs[id][2] = pp;
-          S.outs[id][3] = aligned_key(S.key[i], ps, 0);
-        }
-        id++;
-      }
-    }
-    if (tid == 0) L.nout_pub = tot < NOUT ? tot : NOUT;
-    __syncthreads();
-    // every node's outcome = its chain end's; entries = the first NENT exiting nodes
-    uint32_t ex[NPT], ne = 0;
-    uint8_t oc[NPT];
-#pragma unroll
-    for (uint32_t h = 0; h < NPT; h++) {
-      const uint32_t i = NPT * tid + h;
-      oc[h] = O_DEAD;
-      if (i < nsurv) {
-        const uint32_t t = L.last[i];
-        oc[h] = t == T_DEAD ? O_DEAD : S.out[t];
-      }
-      ex[h] = oc[h] < NOUT ? 1u : 0u;
-      ne += ex[h];
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t h = 0; h < NPT; h++) {
-      const uint32_t i = NPT * tid + h;
-      if (i < nsurv) S.out[i] = oc[h];
-    }
-    uint32_t q = block_scan(L, ne, lane, wave, tot);
-#pragma unroll
-    for (uint32_t h = 0; h < NPT; h++) {
-      const uint32_t i = NPT * tid + h;
-      if (ex[h]) {
-        if (q < NENT) L.ents[q] = S.pos[i] | ((uint32_t)S.rem[i] << 16) | ((uint32_t)oc[h] << 29);
-        q++;
-      }
-    }
-    if (tid == 0) L.nent_pub = tot < NENT ? tot : NENT;
-  }
   __syncthreads();
-
-  // ---- 3. publish the aggregate: lanes store words in parallel, one drain, one flag
-  if (wave == 0) {
-    const uint32_t nent = L.nent_pub, nout = L.nout_pub;
-    if (lane == 0)
-      st_store(rec + R_META, (uint64_t)nent | ((uint64_t)nout << 8) | ((uint64_t)S.overflow << 16));
-    if (lane < (nent + 1) / 2) {
-      const uint32_t q = 2 * lane;
-      st_store(rec + R_ENT0 + lane, (uint64_t)L.ents[q] | (q + 1 < nent ? (uint64_t)L.ents[q + 1] << 32 : 0));
-    }
-    if (lane >= 16 && lane < 16 + nout) {
-      const uint32_t o = lane - 16;
-      st_store(rec + R_OUT0 + 2 * o, S.outs[o][0]);
-      st_store(rec + R_OUT0 + 2 * o + 1, (S.outs[o][1] - ss) | ((S.outs[o][1] - S.outs[o][2]) << 20) |
-                                             (S.outs[o][3] << 32));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(P.fA + seg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (stat_on(P)) {
-      stat_add(P, ST_NSURV, nsurv);
-      if (S.overflow) stat_add(P, ST_OVERFLOW, 1);
-    }
-    stat_phase(P, ST_T_LINK, L.tstamp);
-  }
 }
 
-// ---------------------------------------------------------------- unmask stage
-// Steps 4-5 for the lagged segment (wave 0): input state, own frames, and the
-// (input, output, count) record stores — issued, not waited for. Runs inside
-// the next index stage, while that stage's segment loads are in flight.
-XYWS_DEV void resolve_segment(const st_params& P, st_lds& L, uint32_t lane) {
-  const sv_buf& S = L.sv;
-  const uint64_t seg = S.seg, ss = seg * SEG, se = ss + SEG;
-  const uint32_t nsurv = S.overflow ? 0u : S.nsurv;
-  uint32_t kind;
-  const cstate I = resolve_input(P, L, seg, lane, kind);
-  stat_phase(P, ST_T_INPUT, L.tstamp);
-  if (lane == 0) {
-    const chain_res c = own_chain(P, S, nsurv, ss, se, I);
-    if (c.mode != 2) {
-      uint64_t* rec = P.recs + seg * R_WORDS;
-      store_state(rec + R_CI, I);
-      store_state(rec + R_CO, c.o);
-      st_store(rec + R_NA, c.o.cnt);
-    }
-    L.in = I;
-    L.out = c.o;
-    L.mode = c.mode;
-    L.node_x = c.node;
-    L.rem_x = c.rem;
-    if (stat_on(P)) {
-      stat_add(P, kind == 0 ? ST_EXACT_IN : kind == 1 ? ST_SPEC : ST_FALLBACK, 1);
-      stat_add(P, c.mode == 2 ? ST_MODE2 : ST_MODE1, 1);
-      stat_add(P, ST_SEGS, 1);
-    }
-  }
-  stat_phase(P, ST_T_CHAIN, L.tstamp);
-}
-
-// Step 6 (whole workgroup), after resolve_segment: descriptor ordinals (only
-// when descriptors are wanted), XOR application, then the (input, output)
-// flag and the frame count.
-XYWS_DEV void unmask_segment(const st_params& P, st_lds& L, uint32_t tid, uint32_t lane, uint32_t wave) {
-  const sv_buf& S = L.sv;
-  const uint64_t seg = S.seg;
-  uint64_t* rec = P.recs + seg * R_WORDS;
-  if (tid == 0 && (P.frames || L.mode == 2)) {
-    // header reads (exact chase, descriptors) may straddle into seg+1: its
-    // first bytes must be published (its index stage precedes ours: no cycle)
-    if (seg + 1 < P.nseg) spin_for(P.fA + seg + 1, 1u, P.head + 1, 2u);
-    if (L.mode == 2) {
-      cstate o = L.in;
-      chase_global(P, o, (seg + 1) * SEG);
-      L.out = o;
-      store_state(rec + R_CI, L.in);
-      store_state(rec + R_CO, o);
-      st_store(rec + R_NA, o.cnt);
-    }
-  }
-  if (P.frames && wave == 0) {
-    if (lane == 0) flag_publish(P.fN + seg, 1u);
-    const uint64_t nbase = count_prefix(P, seg, lane);
-    if (lane == 0) {
-      st_store(rec + R_NI, nbase + L.out.cnt);
-      flag_publish(P.fN + seg, 2u);
-      L.nbase = nbase;
-    }
-  } else if (tid == 0) {
-    L.nbase = 0;
-  }
+// ---------------------------------------------------------------- kernels
+template <class G>
+__global__ void __launch_bounds__(G::NT) k_stream_runs(run_params P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
+  lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) L.ticket = atomicAdd(P.head, 1u);
   __syncthreads();
-  const cstate sin = L.in;
-  // the carried-header frame of the batch is described by segment 0
-  if (seg == 0 && tid == 0 && (sin.st & S_HDRCARRY) && !(sin.st & S_PARTIAL)) {
-    hdr_info hh = header_carried(P.base, P.lo, P.hi, P.cin);
-    write_frame(P, 0, P.lo, hh, sin.cov_ps, (int32_t)P.cin->hdr_len);
-  }
-  if (wave == 0) stat_phase(P, ST_F_PREAPPLY, L.tstamp);
-  apply_frames(P, L, &S, seg, sin, L.mode, L.node_x, L.rem_x, L.nbase + sin.cnt, true, tid, true);
-  if (wave == 0) stat_phase(P, ST_T_APPLY, L.tstamp);
-  if (tid == 0) {
-    __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(P.head + 4), L.out.cnt, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    flag_publish(P.fC + seg, 1u);  // (input, output) for fallback inputs of later segments
-  }
-}
-
-// ---------------------------------------------------------------- finish
-// First segment >= from whose pair failed (nseg if none); whole workgroup.
-XYWS_DEV uint64_t next_bad(const st_params& P, st_lds& L, uint64_t from, uint32_t tid) {
-  __syncthreads();
-  if (tid == 0) L.red = 0xFFFFFFFFu;
-  __syncthreads();
-  for (uint64_t b = from; b < P.nseg; b += NT) {
-    const uint64_t j = b + tid;
-    const bool bad = j < P.nseg && flag_load(P.fP + j) == 2u;
-    if (bad) atomicMin(&L.red, (uint32_t)j);
-    if (__syncthreads_or(bad)) break;
-  }
-  const uint32_t r = L.red;
-  __syncthreads();
-  return r == 0xFFFFFFFFu ? P.nseg : r;
-}
-
-// Descriptors of segment j from its (exact) input at ordinal base fb (lane 0).
-XYWS_DEV void emit_segment(const st_params& P, uint64_t j, const cstate& I, uint64_t fb) {
-  const uint64_t se = (j + 1) * SEG, stop = se < P.hi ? se : P.hi;
-  uint64_t X = I.X, ord = fb;
-  if (I.st & S_PARTIAL) return;
-  while (X < stop && ord < P.cap) {
-    hdr_info hh = header_safe(P, X);
-    if (!hh.hlen) return;
-    const uint64_t ps = X + hh.hlen;
-    write_frame(P, ord++, X, hh, ps, 0);
-    X = sat_add(ps, hh.plen);
-  }
-}
-
-// The last workgroup to exit: repair mis-speculated segments, then the frame
-// count and the carry out. Whole workgroup; every other workgroup has exited
-// (its stores written back by its release fence).
-XYWS_DEV void finish(const st_params& P, st_lds& L, uint32_t tid) {
-  const uint64_t nseg = P.nseg;
-  int64_t delta = 0;
-  cstate E = load_state(rec_of(P, nseg - 1) + R_CO);
-  if (flag_load(P.head + 3)) {  // some pair failed: repair in order from the first
-    uint64_t k = next_bad(P, L, 1, tid);
-    if (k < nseg) E = load_state(rec_of(P, k - 1) + R_CO);
-    while (k < nseg) {
-      const cstate W = load_state(rec_of(P, k) + R_CI);
-      const uint64_t old_n = st_load(rec_of(P, k) + R_NA);
-      const uint64_t fb0 = P.frames ? st_load(rec_of(P, k) + R_NI) - old_n : 0;
-      if (same_state(W, E)) {  // k's input is exact again: outputs stand until the next bad pair
-        const uint64_t nk = next_bad(P, L, k + 1, tid);
-        if (delta != 0 && P.frames && tid == 0) {  // ordinals shifted: rewrite their descriptors
-          for (uint64_t j = k; j < nk; j++) {
-            const uint64_t nj = st_load(rec_of(P, j) + R_NA);
-            const uint64_t fbj = st_load(rec_of(P, j) + R_NI) - nj + (uint64_t)delta;
-            if (fbj >= P.cap) break;
-            emit_segment(P, j, load_state(rec_of(P, j) + R_CI), fbj);
+  const uint32_t run = L.ticket;
+  if (run >= P.nruns) return;
+  uint64_t* rec = P.rec + (uint64_t)run * R_WORDS;
+  if (tid == 0) st_store(rec + R_ECNT, 0);  // no descriptors unless k_stream_finish plans them
+  const uint64_t rng_end = run + 1 < P.nruns ? (uint64_t)(run + 1) * P.spr * G::SEG : NONE;
+  seg_io<G> io;
+  uint64_t t0 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t wlo, s0;
+  bool in_lds = false;
+  if (run == 0) {
+    if (tid == 0) {
+      uint64_t c0;
+      L.S = initial_state(P, c0);
+      L.cnt = c0;
+      st_store(rec + R_H, P.lo);
+      st_store(rec + R_W, P.lo);
+      put_state(rec + R_S0, L.S);
+      st_store(rec + R_HEAD, c0);
+    }
+    wlo = P.lo;
+    s0 = 0;
+  } else {
+    find_entry(P, L, io, tid, run);
+    if (tid == 0) {
+      const uint64_t q = L.aux0, seg_q = L.aux1;
+      const uint64_t ss = seg_q * G::SEG;
+      uint64_t h = NONE, W = NONE, hc = 0;
+      cstate S;
+      S.X = 0; S.cov_ps = 0; S.cov_start = 0; S.cov_kw = 0; S.cov_key = 0; S.st = S_NOCOV; S.pad = 0;
+      if (q != NONE) {
+        const hdr_info hq = hdr_at(P, L, ss, q, NONE);
+        h = (hq.hlen == 2 || hq.hlen == 6) ? sat_add(q + hq.hlen, hq.plen) : q;
+        const hdr_info hh = h < P.hi ? hdr_at(P, L, ss, h, NONE) : hq;
+        if (h >= rng_end || h >= P.hi || !hh.hlen) {
+          h = NONE;
+        } else {
+          W = (h + hh.hlen + 15) & ~15ull;
+          // frames starting below W: parsed here, from bytes nobody writes yet
+          S = frame_state(h, hh);
+          hc = 1;
+          while (S.X < W && S.X < P.hi) {
+            const hdr_info hx = hdr_at(P, L, ss, S.X, NONE);
+            if (!hx.hlen) { S.st |= S_PARTIAL; break; }
+            S = frame_state(S.X, hx);
+            hc++;
           }
         }
-        if (nk >= nseg) { E = load_state(rec_of(P, nseg - 1) + R_CO); break; }
-        k = nk;
-        E = load_state(rec_of(P, k - 1) + R_CO);
-        continue;
       }
-      // undo the frames of the wrong input (its chain's header bytes are intact)
-      if (stat_on(P)) stat_add(P, ST_REPAIR, 1);
-      apply_frames(P, L, nullptr, k, W, 2, 0, 0, 0, false, tid);
-      __threadfence();
-      __syncthreads();
-      // redo from the exact input
-      if (tid == 0) {
-        cstate o = E;
-        o.cnt = 0;
-        chase_global(P, o, (k + 1) * SEG);
-        L.out = o;
-      }
-      __syncthreads();
-      const cstate o = L.out;
-      apply_frames(P, L, nullptr, k, E, 2, 0, 0, fb0 + (uint64_t)delta, true, tid);
-      __threadfence();
-      __syncthreads();
-      delta += (int64_t)o.cnt - (int64_t)old_n;
-      E = o;
-      k++;
+      st_store(rec + R_H, h);
+      st_store(rec + R_W, W);
+      put_state(rec + R_S0, S);
+      st_store(rec + R_HEAD, hc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(P.flags + run, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      L.S = S;
+      L.cnt = hc;
+      L.aux2 = h == NONE ? NONE : W;
+      stat_add(P, ST_RUNS, 1);
+      if (h == NONE) stat_add(P, ST_NONE, 1);
+      if (stats_on(P)) stat_add(P, ST_T_PRO, __builtin_amdgcn_s_memtime() - t0);
     }
+    __syncthreads();
+    if (L.aux2 == NONE) return;  // no entry: the chain of an earlier run covers this range
+    wlo = L.aux2;
+    s0 = wlo / G::SEG;
+    in_lds = s0 == L.aux1;
   }
   if (tid == 0) {
-    const uint64_t total = __hip_atomic_load(reinterpret_cast<uint64_t*>(P.head + 4), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT) + (uint64_t)delta;
-    const cstate o = E;
+    L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.first_after = NONE;
+    L.known = rng_end == NONE;
+    L.hn = NONE; L.Wn = NONE; L.succ = P.nruns;
+  }
+  __syncthreads();
+  uint64_t t1 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
+  run_chain(P, L, io, tid, s0, in_lds, wlo, rng_end, run);
+  if (tid == 0) {
+    const bool ok = L.succ >= P.nruns || (L.past && L.ok);
+    st_store(rec + R_OK, (uint64_t)(ok ? 1u : 0u) | ((uint64_t)L.succ << 32));
+    st_store(rec + R_HN, L.hn);
+    st_store(rec + R_WN, L.Wn);
+    st_store(rec + R_CNT, L.cnt);
+    st_store(rec + R_TAIL, L.tail);
+    st_store(rec + R_FIRST, L.first_after);
+    put_state(rec + R_F0, L.S);
+    if (!ok) stat_add(P, ST_BAD, 1);
+    stat_add(P, ST_FRAMES, L.cnt);
+    if (stats_on(P)) stat_add(P, ST_T_MAIN, __builtin_amdgcn_s_memtime() - t1);
+  }
+}
+
+// Walk the runs from run 0 along their successors, repairing every boundary
+// whose chain did not land on the successor's entry, then the frame count, the
+// carry and the descriptor plan (one workgroup; every run has exited).
+template <class G>
+__global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
+  lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
+  const uint32_t tid = threadIdx.x;
+  seg_io<G> io;
+  // lane-0 walk state: aux0 = current run, aux2 = ordinal base; B/bcnt/bfirst:
+  // the exact state handed to a repaired run, the frames its predecessor chased
+  // into it and its first node; repaired: the current run's results are the
+  // redo's (left in L by run_chain)
+  // Fast path (every run with an entry landed exactly on its successor's
+  // entry: the usual case): frame counts, descriptor ordinals and the final
+  // state by a block-wide scan over the run records, no serial walk.
+  {
+    uint64_t* scr = reinterpret_cast<uint64_t*>(L.seg);  // scratch: wave totals
+    const uint32_t lane = tid & 63u, wave = tid >> 6;
+    uint64_t carry = 0;
+    uint32_t bad = 0, last = 0;
+    for (uint32_t t0 = 0; t0 < P.nruns; t0 += G::NT) {
+      const uint32_t r = t0 + tid;
+      const uint64_t* rec = P.rec + (uint64_t)r * R_WORDS;
+      const uint64_t h = r < P.nruns ? st_load(rec + R_H) : NONE;
+      const bool vis = r < P.nruns && (r == 0 || h != NONE);
+      const uint64_t cnt = vis ? st_load(rec + R_CNT) : 0;
+      if (vis && !(st_load(rec + R_OK) & 1u)) bad = 1;
+      if (vis) last = r;
+      uint64_t x = cnt;  // wave inclusive scan
+#pragma unroll
+      for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (lane == 63) scr[wave] = x;
+      __syncthreads();
+      uint64_t wb = 0, tot = 0;
+      for (uint32_t w = 0; w < G::NT / 64; w++) {
+        const uint64_t v = scr[w];
+        if (w < wave) wb += v;
+        tot += v;
+      }
+      if (vis) {
+        uint64_t* rw = P.rec + (uint64_t)r * R_WORDS;
+        st_store(rw + R_EFROM, h);
+        st_store(rw + R_ECNT, cnt);
+        st_store(rw + R_EORD, carry + wb + x - cnt);
+        st_store(rw + R_ECARRY, r == 0 ? 1u : 0u);
+      }
+      carry += tot;
+      __syncthreads();
+    }
+    const bool any_bad = __syncthreads_or(bad);
+    if (tid == 0) L.aux1 = 0;
+    __syncthreads();
+    if (last) atomicMax(reinterpret_cast<unsigned long long*>(&L.aux1), (unsigned long long)last);
+    __syncthreads();
+    if (!any_bad) {
+      if (tid == 0) {
+        L.aux2 = carry;
+        L.S = get_state(P.rec + L.aux1 * R_WORDS + R_F0);
+      }
+      __syncthreads();
+    }
+    if (any_bad) stat_add(P, ST_BAD, 0);
+    if (tid == 0) L.act = any_bad ? 1u : 0u;
+    __syncthreads();
+  }
+  if (L.act) {
+  if (tid == 0) { L.aux0 = 0; L.aux2 = 0; L.repaired = 0; }
+  __syncthreads();
+  for (uint32_t guard = 0; guard <= 2 * P.nruns + 2; guard++) {
+    if (tid == 0) {
+      const uint32_t r = (uint32_t)L.aux0;
+      uint64_t* rec = P.rec + (uint64_t)r * R_WORDS;
+      uint64_t ok, succ, cnt, tail, first, efrom;
+      cstate F;
+      if (L.repaired) {  // results of the redo (left in L by run_chain)
+        ok = L.succ >= P.nruns || (L.past && L.ok);
+        succ = L.succ;
+        cnt = L.bcnt + L.cnt;
+        tail = L.tail;
+        first = L.first_after;
+        F = L.S;
+        efrom = L.bfirst;
+      } else {
+        const uint64_t w = st_load(rec + R_OK);
+        ok = w & 1u;
+        succ = w >> 32;
+        cnt = st_load(rec + R_CNT);
+        tail = st_load(rec + R_TAIL);
+        first = st_load(rec + R_FIRST);
+        F = get_state(rec + R_F0);
+        efrom = st_load(rec + R_H);
+      }
+      st_store(rec + R_EFROM, efrom);
+      st_store(rec + R_ECNT, cnt);
+      st_store(rec + R_EORD, L.aux2);
+      st_store(rec + R_ECARRY, L.repaired ? 0u : (r == 0 ? 1u : 0u));
+      L.aux2 += cnt;
+      if (succ >= P.nruns) {
+        L.act = 0;  // done
+        L.S = F;
+      } else if (ok) {
+        L.act = 1;  // next run as recorded
+        L.aux0 = succ;
+        L.repaired = 0;
+      } else {
+        // boundary `succ` mis-speculated: undo its run, redo from our exact chain
+        stat_add(P, ST_REPAIR, 1);
+        const uint64_t* rs = P.rec + succ * R_WORDS;
+        L.B = F;
+        L.bcnt = tail;
+        L.bfirst = first != NONE ? first : F.X;
+        L.act = 2;
+        L.aux0 = succ;
+        L.S = get_state(rs + R_S0);
+        L.S.st &= ~S_CUT;
+        L.hn = st_load(rs + R_HN);
+        L.Wn = st_load(rs + R_WN);
+        L.succ = st_load(rs + R_OK) >> 32;
+        L.known = 1; L.cnt = 0; L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0;
+        L.first_after = NONE;
+        L.best = 0;
+      }
+    }
+    __syncthreads();
+    if (L.act == 0) break;
+    if (L.act == 1) continue;
+    // undo: replay the mis-speculated run exactly as it ran
+    const uint64_t* rs = P.rec + L.aux0 * R_WORDS;
+    const uint64_t W = st_load(rs + R_W);
+    const uint64_t hn = L.hn, Wn = L.Wn, succ = L.succ;
+    io.pf = NONE;
+    run_chain(P, L, io, tid, W / G::SEG, false, W, NONE, 0);
+    __threadfence();  // the undo's stores are visible to the redo's loads
+    __syncthreads();
+    // redo from the exact state, same successor
+    if (tid == 0) {
+      L.S = L.B;
+      L.S.st &= ~S_CUT;
+      L.hn = hn; L.Wn = Wn; L.succ = succ;
+      L.known = 1; L.cnt = 0; L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0;
+      L.first_after = NONE;
+      L.repaired = 1;
+    }
+    __syncthreads();
+    io.pf = NONE;
+    run_chain(P, L, io, tid, W / G::SEG, false, W, NONE, 0);
+    __threadfence();
+    __syncthreads();
+  }
+  }  // serial walk with repairs
+  if (tid == 0) {
+    const uint64_t total = L.aux2;
+    const cstate o = L.S;
     if (P.nframes) *P.nframes = total;
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(P.head + 2), total, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
     if (P.cout) {
       const uint64_t lo = P.lo, hi = P.hi;
       xyws_carry c;
@@ -1274,8 +958,7 @@ XYWS_DEV void finish(const st_params& P, st_lds& L, uint32_t tid) {
           c.phase = P.cin->phase + (hi - lo);
           for (int i = 0; i < 4; i++) c.key[i] = P.cin->key[i];
         } else {
-          const hdr_info hh = (o.st & S_HDRCARRY) ? header_carried(P.base, lo, hi, P.cin)
-                                                  : header_safe(P, o.cov_start);
+          const hdr_info hh = (o.st & S_HDRCARRY) ? header_carried(P) : hdr_global(P, o.cov_start, NONE);
           c.payload_remaining = hh.plen - (hi - o.cov_ps);
           c.phase = hi - o.cov_ps;
           c.key[0] = (uint8_t)hh.key; c.key[1] = (uint8_t)(hh.key >> 8);
@@ -1287,41 +970,53 @@ XYWS_DEV void finish(const st_params& P, st_lds& L, uint32_t tid) {
   }
 }
 
-// ---------------------------------------------------------------- kernels
-// One workgroup per segment, in ticket order (so every segment a workgroup
-// waits for belongs to a workgroup that started earlier). Straight-line: index,
-// resolve (wave 0), unmask. 4 workgroups = 16 waves per CU (<= 128 VGPRs,
-// <= 40 KiB LDS each): while some wait on memory or on predecessors, others run.
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) k_stream_fused(st_params P) {
-  st_lds& L = g_L;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  if (tid == 0) {
-    L.seg_id = atomicAdd(P.head, 1u);
-    L.tstamp = stat_on(P) ? __builtin_amdgcn_s_memtime() : 0;
-  }
-  __syncthreads();
-  const uint64_t seg = L.seg_id;
-  index_segment(P, L, seg, tid, lane, wave);
-  if (wave == 0) resolve_segment(P, L, lane);
-  __syncthreads();
-  unmask_segment(P, L, tid, lane, wave);
+XYWS_DEV void write_frame(const run_params& P, uint64_t ord, uint64_t start, const hdr_info& h,
+                          uint64_t ps, int32_t hdr_shift) {
+  xyws_frame f;
+  f.frame_off = (int64_t)(start - P.lo) - hdr_shift;
+  f.payload_off = (int64_t)(ps - P.lo);
+  f.payload_len = h.plen;
+  f.key[0] = (uint8_t)h.key; f.key[1] = (uint8_t)(h.key >> 8);
+  f.key[2] = (uint8_t)(h.key >> 16); f.key[3] = (uint8_t)(h.key >> 24);
+  f.flags = h.flags;
+  f.hdr_len = (uint8_t)h.hlen;
+  f.status = (uint8_t)(h.status | (sat_add(ps, h.plen) > P.hi ? XYWS_ST_PAYLOAD_INCOMPLETE : 0));
+  f.reserved = 0;
+  P.frames[ord] = f;
 }
 
-// Pair checks after the decode: segment k's assumed input against segment
-// k-1's output (one thread per pair; the kernel boundary orders the records).
-__global__ void __launch_bounds__(256) k_stream_pairs(st_params P) {
-  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x + 1;
-  if (k >= P.nseg) return;
-  const bool ok = same_state(load_state(rec_of(P, k) + R_CI), load_state(rec_of(P, k - 1) + R_CO));
-  P.fP[k] = ok ? 1u : 2u;
-  if (!ok) {
-    atomicOr(P.head + 3, 1u);
-    if (stat_on(P)) atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + ST_BADPAIR, 1ull);
+// Descriptors: one lane per run re-chases the run's frames (headers are never
+// modified by the decode) and writes them at their ordinals.
+__global__ void __launch_bounds__(64) k_stream_emit(run_params P) {
+  const uint32_t r = blockIdx.x;
+  if (threadIdx.x != 0 || r >= P.nruns) return;
+  const uint64_t* rec = P.rec + (uint64_t)r * R_WORDS;
+  uint64_t ord = st_load(rec + R_EORD);
+  const uint64_t n = st_load(rec + R_ECNT);
+  if (n == 0 || ord >= P.cap) return;
+  const uint64_t end = ord + n < P.cap ? ord + n : P.cap;
+  uint64_t X = st_load(rec + R_EFROM);
+  if (st_load(rec + R_ECARRY)) {  // run 0: the carried-header frame comes first
+    X = P.lo;
+    if (!P.cin->payload_remaining && P.cin->hdr_len) {
+      const hdr_info hh = header_carried(P);
+      if (hh.hlen) {
+        const uint64_t ps = P.lo + (hh.hlen - P.cin->hdr_len);
+        write_frame(P, ord++, P.lo, hh, ps, (int32_t)P.cin->hdr_len);
+        X = sat_add(ps, hh.plen);
+      }
+    } else if (P.cin->payload_remaining) {
+      X = sat_add(P.lo, P.cin->payload_remaining);
+    }
+  }
+  while (ord < end && X < P.hi) {
+    const hdr_info hh = hdr_global(P, X, NONE);
+    if (!hh.hlen) break;
+    const uint64_t ps = X + hh.hlen;
+    write_frame(P, ord++, X, hh, ps, 0);
+    X = sat_add(ps, hh.plen);
   }
 }
-
-// Repairs (if any pair failed), the frame count and the carry out.
-__global__ void __launch_bounds__(NT) k_stream_finish(st_params P) { finish(P, g_L, threadIdx.x); }
 
 // Empty batch: the state passes through unchanged.
 __global__ void k_stream_empty(const xyws_carry* cin, xyws_carry* cout, uint64_t* nframes) {
@@ -1335,28 +1030,50 @@ __global__ void k_stream_empty(const xyws_carry* cin, xyws_carry* cout, uint64_t
   }
 }
 
-constexpr uint64_t HEAD_BYTES = 512;  // [0] ticket .. [5]; [64..128) carry snapshot; [128..384) stats
+constexpr uint64_t HEAD_BYTES = 512;  // [0] ticket, [1] error, [2..3] total; [64..128) carry; [128..384) stats
+
+template <class G>
+int launch_runs(const run_params& P, hipStream_t stream) {
+  static bool attr_set = false;
+  const size_t lds = sizeof(lds_t<G>);
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)k_stream_runs<G>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_stream_finish<G>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return XYWS_ERR_HIP;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k_stream_runs<G>, dim3(P.nruns), dim3(G::NT), lds, stream, P);
+  hipLaunchKernelGGL(k_stream_finish<G>, dim3(1), dim3(G::NT), lds, stream, P);
+  if (P.frames && P.cap) hipLaunchKernelGGL(k_stream_emit, dim3(P.nruns), dim3(64), 0, stream, P);
+  return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
+}
 
 }  // namespace
 
-void stream_scratch_init(stream_scratch* s) {
+void stream_scratch_init(stream_scratch* s, int device) {
   s->mem = nullptr;
   s->bytes = 0;
-  s->max_tiles = 0;
+  s->max_runs = 0;
+  s->ncu = 256;
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && n > 0)
+    s->ncu = n;
 }
 
 void stream_scratch_free(stream_scratch* s) {
   if (s->mem) (void)hipFree(s->mem);
   s->mem = nullptr;
   s->bytes = 0;
-  s->max_tiles = 0;
+  s->max_runs = 0;
 }
 
-static uint64_t flags_bytes(uint64_t n) { return (4 * n * 4 + 255) & ~255ull; }  // fA fC fN fP
+static uint64_t flags_bytes(uint64_t n) { return (4 * n + 255) & ~255ull; }
 
-static int scratch_grow(stream_scratch* s, uint64_t segs) {
-  if (s->mem && segs <= s->max_tiles) return XYWS_OK;
-  const uint64_t want = segs < 64 ? 64 : segs;
+static int scratch_grow(stream_scratch* s, uint64_t runs) {
+  if (s->mem && runs <= s->max_runs) return XYWS_OK;
+  const uint64_t want = runs < 64 ? 64 : runs;
   const uint64_t bytes = HEAD_BYTES + flags_bytes(want) + want * R_WORDS * 8;
   void* m = nullptr;
   if (hipMalloc(&m, bytes) != hipSuccess) return XYWS_ERR_NOMEM;
@@ -1366,12 +1083,16 @@ static int scratch_grow(stream_scratch* s, uint64_t segs) {
   }
   s->mem = m;
   s->bytes = bytes;
-  s->max_tiles = want;
+  s->max_runs = want;
   return hipMemset(m, 0, HEAD_BYTES) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
 
 int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
-  return scratch_grow(s, (max_batch_bytes + 15 + SEG - 1) / SEG + 1);
+  // production geometry: at most one run per CU (the small-segment test mode
+  // grows scratch lazily)
+  const uint64_t nseg = (max_batch_bytes + 15 + G_PROD::SEG - 1) / G_PROD::SEG;
+  const uint64_t r = (uint64_t)s->ncu * RUNS_PER_CU, maxr = r < MAX_RUNS ? r : MAX_RUNS;
+  return scratch_grow(s, nseg < maxr ? nseg + 1 : maxr);
 }
 
 int stream_scratch_stats(stream_scratch* s, uint64_t out[32]) {
@@ -1395,31 +1116,37 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     hipLaunchKernelGGL(k_stream_empty, dim3(1), dim3(64), 0, stream, cin, cout, nframes);
     return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
   }
-  const uint64_t nseg = (hi + SEG - 1) / SEG;
+  const bool small = (opts & XYWS_OPT_SMALL_SEG) != 0;
+  const uint64_t seg = small ? G_SMALL::SEG : G_PROD::SEG;
+  const uint64_t nseg = (hi + seg - 1) / seg;
+  uint64_t nruns, spr;
+  if (small) {
+    nruns = nseg;
+    spr = 1;
+  } else {
+    const uint64_t r = (uint64_t)s->ncu * RUNS_PER_CU, maxr = r < MAX_RUNS ? r : MAX_RUNS;
+    spr = (nseg + maxr - 1) / maxr;
+    nruns = (nseg + spr - 1) / spr;
+  }
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(stream, &cs);
-  if (nseg > s->max_tiles || !s->mem) {
+  if (nruns > s->max_runs || !s->mem) {
     if (cs != hipStreamCaptureStatusNone) return XYWS_ERR_CAPACITY;
-    const int rc = scratch_grow(s, nseg);
+    const int rc = scratch_grow(s, nruns);
     if (rc) return rc;
   }
   uint8_t* m = static_cast<uint8_t*>(s->mem);
-  st_params P;
+  run_params P;
   P.base = base; P.lo = lo; P.hi = hi; P.nseg = nseg;
+  P.nruns = (uint32_t)nruns; P.spr = (uint32_t)spr;
   P.cout = cout; P.frames = frames; P.cap = cap; P.nframes = nframes;
   P.head = reinterpret_cast<uint32_t*>(m);
-  uint32_t* fl = reinterpret_cast<uint32_t*>(m + HEAD_BYTES);
-  P.fA = fl;
-  P.fC = fl + nseg;
-  P.fN = fl + 2 * nseg;
-  P.fP = fl + 3 * nseg;
-  P.recs = reinterpret_cast<uint64_t*>(m + HEAD_BYTES + flags_bytes(s->max_tiles));
+  P.flags = reinterpret_cast<uint32_t*>(m + HEAD_BYTES);
+  P.rec = reinterpret_cast<uint64_t*>(m + HEAD_BYTES + flags_bytes(s->max_runs));
   P.opts = opts;
-  // Ticket, exit counter, bad-pair word, total and flags zeroed every call (the
-  // error word [1] is sticky until read back). The carry is snapshotted first:
-  // dev_carry_in may alias dev_carry_out, which the finishing workgroup writes.
+  // Ticket and total zeroed every call (the error word [1] is sticky until read
+  // back). The carry is snapshotted first: dev_carry_in may alias dev_carry_out.
   xyws_carry* snap = reinterpret_cast<xyws_carry*>(m + 64);
-  if (hipMemsetAsync(P.head + 2, 0, 16, stream) != hipSuccess) return XYWS_ERR_HIP;  // [2..5]
   if (hipMemsetAsync(P.head, 0, 4, stream) != hipSuccess) return XYWS_ERR_HIP;
   if ((opts & XYWS_OPT_STATS) && hipMemsetAsync(m + 128, 0, 256, stream) != hipSuccess) return XYWS_ERR_HIP;
   if (cin) {
@@ -1429,10 +1156,6 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     return XYWS_ERR_HIP;
   }
   P.cin = snap;
-  if (hipMemsetAsync(fl, 0, (4 * nseg * 4 + 15) & ~15ull, stream) != hipSuccess) return XYWS_ERR_HIP;
-  hipLaunchKernelGGL(k_stream_fused, dim3((uint32_t)nseg), dim3(NT), 0, stream, P);
-  if (nseg > 1)
-    hipLaunchKernelGGL(k_stream_pairs, dim3((uint32_t)((nseg - 1 + 255) / 256)), dim3(256), 0, stream, P);
-  hipLaunchKernelGGL(k_stream_finish, dim3(1), dim3(NT), 0, stream, P);
-  return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
+  if (hipMemsetAsync(P.flags, 0, (4 * nruns + 15) & ~15ull, stream) != hipSuccess) return XYWS_ERR_HIP;
+  return small ? launch_runs<G_SMALL>(P, stream) : launch_runs<G_PROD>(P, stream);
 }

@@ -219,12 +219,15 @@ class frame_decoder:
     back-to-back batches and unmask payloads in place, carrying a frame or header
     cut by a batch end into the next batch (xyws_decode_stream)."""
 
-    def __init__(self, device=None, serial=False, parse_only=False):
+    def __init__(self, device=None, serial=False, parse_only=False, small_segments=False):
+        """serial: the one-lane exact chase (XYWS_OPT_SERIAL_SCAN). small_segments:
+        test geometry of the run-parallel decoder (1 KiB runs), so that small
+        inputs cross many run boundaries (speculated entries and their repair)."""
         import torch
         self.ctx = context(device)
         self.device = torch.device("cuda", self.ctx.device)
         self.carry_t = torch.zeros(64, dtype=torch.uint8, device=self.device)
-        self.opts = (4 if serial else 0) | (1 if parse_only else 0)
+        self.opts = (4 if serial else 0) | (1 if parse_only else 0) | (0x200 if small_segments else 0)
 
     def reset(self):
         self.carry_t.zero_()
