@@ -19,6 +19,7 @@ from xynet_amd import websocket as ws  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "random_frames_40"
 mode = sys.argv[2] if len(sys.argv) > 2 else "fused"
+split = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 kw = {"fused": {}, "runs1k": {"small_segments": True}, "serial": {"serial": True}}[mode]
 src = streams.case_bytes(name)
 orc = Oracle()
@@ -27,7 +28,15 @@ ofr, oc, on = orc.decode_stream(ob)
 t = torch.frombuffer(bytearray(src), dtype=torch.uint8).cuda()
 dec = ws.frame_decoder(**kw)
 dec.opts |= 0x100
-r = dec.decode(t, cap=on + 4)
+if split:
+    a = t[:split].clone()
+    b = t[split:].clone()
+    ra = dec.decode(a, cap=on + 4)
+    print("carry after piece 1:", list(bytes(dec.carry())[:40]))
+    r = dec.decode(b, cap=on + 4)
+    t = torch.cat([a, b])
+else:
+    r = dec.decode(t, cap=on + 4)
 out = (C.c_uint64 * 32)()
 dec.ctx.L.xyws_debug_stats(dec.ctx.h, out)
 print("len", len(src), "nframes gpu", r.nframes, "oracle", on)

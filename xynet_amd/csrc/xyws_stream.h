@@ -24,6 +24,7 @@ int stream_scratch_stats(stream_scratch* s, uint64_t out[32]);
 #define XYWS_OPT_SMALL_SEG 0x200u  // 1 KiB segments, one per run: exercises run-boundary
                                    // speculation and repair on small test inputs
 #define XYWS_OPT_NO_STORE 0x20000u // diagnostics: decode without writing (timing split only)
+#define XYWS_OPT_WG512 0x40000u    // two 512-thread workgroups per CU, 64 KiB segments
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
                         const xyws_carry* cin, xyws_carry* cout, xyws_frame* frames, uint64_t cap,
                         uint64_t* nframes, uint32_t opts, hipStream_t stream);

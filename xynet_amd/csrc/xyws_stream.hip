@@ -70,7 +70,7 @@ constexpr uint32_t OOB = 0x80000000u; // buffer offset past every range: load 0,
 constexpr int AUX_NT = 2;             // buffer cache policy: nontemporal
 constexpr uint64_t PLEN_SPEC_MAX = 1ull << 46;
 constexpr uint32_t MAX_RUNS = 1024;
-constexpr uint32_t RUNS_PER_CU = 2;   // workgroups resident per CU (LDS: two ~72 KiB blocks)
+
 
 // chase-state bits
 constexpr uint32_t S_PARTIAL = 1;    // header at X incomplete at the batch end
@@ -84,7 +84,8 @@ template <uint32_t NT_, uint32_t CH_>
 struct geom {
   static constexpr uint32_t NT = NT_, CH = CH_, SEG = NT_ * CH_ * 16;
 };
-using G_PROD = geom<512, 8>;   // 64 KiB segments, 8 waves, two workgroups per CU
+using G_PROD = geom<1024, 8>;  // 128 KiB segments, 16 waves, one workgroup per CU (default)
+using G_PROD2 = geom<512, 8>;  // 64 KiB segments, 8 waves, two workgroups per CU (XYWS_OPT_WG512)
 using G_SMALL = geom<64, 1>;   // 1 KiB segments, one wave (XYWS_OPT_SMALL_SEG)
 
 struct fent {
@@ -376,11 +377,11 @@ XYWS_DEV u32x4 chunk_xor(const lds_t<G>& L, uint32_t nfl, uint32_t g, uint32_t a
 // the pass start, then frames parsed from X, up to FCAP entries. Sets
 // pass_hi: the chunks below it are final for this pass.
 template <class G>
-XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t lo_c) {
+XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t lo_c, uint32_t keep) {
   const uint64_t se = ss + G::SEG;
   cstate S = L.S;
-  uint32_t n = 0;
-  if (!(S.st & (S_NOCOV | S_PARTCARRY)) && S.X > ss + lo_c) {
+  uint32_t n = keep;  // entries carried from the previous pass (they include the covering frame)
+  if (!keep && !(S.st & (S_NOCOV | S_PARTCARRY)) && S.X > ss + lo_c) {
     fent e;
     e.start = 0;
     e.ps = clamp_rel(S.cov_ps, ss);
@@ -522,9 +523,9 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
     if (nx < P.hi && nx < wlim && !fin0 && io.pf != s + 1) io.issue(P, s + 1, tid);
     XYWS_STAMP(acc_pf);
     const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, s);
-    uint32_t lo_c = 0;
+    uint32_t lo_c = 0, keep = 0;
     for (;;) {
-      if (tid == 0) chase_pass(P, L, ss, lo_c);
+      if (tid == 0) chase_pass(P, L, ss, lo_c, keep);
       XYWS_STAMP(acc_cp);
       __syncthreads();
       XYWS_STAMP(acc_sync);
@@ -590,6 +591,14 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
       XYWS_STAMP(acc_xor);
       if (hi_c >= G::SEG) break;
       __syncthreads();  // the list is rebuilt for the next pass
+      if (tid == 0) {   // entries reaching past hi_c (tiny frames can share its chunk) carry over
+        uint32_t c = nfl;
+        while (c > 0 && L.fl[c - 1].end > hi_c) c--;
+        for (uint32_t i = c; i < nfl; i++) L.fl[i - c] = L.fl[i];
+        L.aux2 = nfl - c;
+      }
+      __syncthreads();
+      keep = (uint32_t)L.aux2;
       lo_c = hi_c;
     }
     // continue while bytes below the write limit remain
@@ -1090,8 +1099,8 @@ static int scratch_grow(stream_scratch* s, uint64_t runs) {
 int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
   // production geometry: at most one run per CU (the small-segment test mode
   // grows scratch lazily)
-  const uint64_t nseg = (max_batch_bytes + 15 + G_PROD::SEG - 1) / G_PROD::SEG;
-  const uint64_t r = (uint64_t)s->ncu * RUNS_PER_CU, maxr = r < MAX_RUNS ? r : MAX_RUNS;
+  const uint64_t nseg = (max_batch_bytes + 15 + G_PROD2::SEG - 1) / G_PROD2::SEG;
+  const uint64_t r = (uint64_t)s->ncu * 2, maxr = r < MAX_RUNS ? r : MAX_RUNS;
   return scratch_grow(s, nseg < maxr ? nseg + 1 : maxr);
 }
 
@@ -1117,14 +1126,15 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
   }
   const bool small = (opts & XYWS_OPT_SMALL_SEG) != 0;
-  const uint64_t seg = small ? G_SMALL::SEG : G_PROD::SEG;
+  const bool wg512 = !small && (opts & XYWS_OPT_WG512) != 0;
+  const uint64_t seg = small ? G_SMALL::SEG : wg512 ? G_PROD2::SEG : G_PROD::SEG;
   const uint64_t nseg = (hi + seg - 1) / seg;
   uint64_t nruns, spr;
   if (small) {
     nruns = nseg;
     spr = 1;
   } else {
-    const uint64_t r = (uint64_t)s->ncu * RUNS_PER_CU, maxr = r < MAX_RUNS ? r : MAX_RUNS;
+    const uint64_t r = (uint64_t)s->ncu * (wg512 ? 2u : 1u), maxr = r < MAX_RUNS ? r : MAX_RUNS;
     spr = (nseg + maxr - 1) / maxr;
     nruns = (nseg + spr - 1) / spr;
   }
@@ -1157,5 +1167,6 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   }
   P.cin = snap;
   if (hipMemsetAsync(P.flags, 0, (4 * nruns + 15) & ~15ull, stream) != hipSuccess) return XYWS_ERR_HIP;
-  return small ? launch_runs<G_SMALL>(P, stream) : launch_runs<G_PROD>(P, stream);
+  return small ? launch_runs<G_SMALL>(P, stream)
+               : wg512 ? launch_runs<G_PROD2>(P, stream) : launch_runs<G_PROD>(P, stream);
 }
