@@ -46,7 +46,8 @@
 // own and which never waits, so the lowest ticket always progresses. Header
 // bytes are read only where no other workgroup writes: below the successor's W
 // (a header that would cross it stops the chase, "cut"), or in the run's own
-// range. Flags and the ticket are zeroed by hipMemsetAsync before every launch;
+// range. Flags and the ticket are zeroed when scratch is allocated and reset by
+// k_stream_finish after every call (so a captured graph replays correctly);
 // spins are bounded and report through the device error word.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -64,7 +65,7 @@ constexpr uint32_t PAD = 32;          // LDS bytes after the segment (5-dword he
 // (~5e-10 per random position), a 126-form one 0xFE/0x7E (~1.4e-4), a 7-bit
 // one just a plausible first byte (~1.7e-2); each further plausible header
 // multiplies by ~1.8e-2. Short hops mostly stay in LDS; long ones are memory reads.
-constexpr uint32_t KHDR_127 = 2, KHDR_126 = 4, KHDR_7 = 6;
+constexpr uint32_t KHDR_127 = 1, KHDR_126 = 4, KHDR_7 = 6;
 constexpr uint32_t SPIN = 1u << 24;   // bounded spins (s_sleep 2 each: ~1 s)
 constexpr uint32_t OOB = 0x80000000u; // buffer offset past every range: load 0, store dropped
 constexpr int AUX_NT = 2;             // buffer cache policy: nontemporal
@@ -80,17 +81,22 @@ constexpr uint32_t S_HDRCARRY = 8;   // covering frame's header began in the pre
 constexpr uint32_t S_PARTCARRY = 16; // the carried partial header is still incomplete
 constexpr uint32_t S_CUT = 32;       // header at X crosses the write limit (left to the repair)
 
-template <uint32_t NT_, uint32_t CH_>
+template <uint32_t NT_, uint32_t CH_, uint32_t WPE_>
 struct geom {
-  static constexpr uint32_t NT = NT_, CH = CH_, SEG = NT_ * CH_ * 16;
+  // threads, 16-byte chunks per thread, waves per SIMD the decode kernel must
+  // fit (register budget 512 / WPE)
+  static constexpr uint32_t NT = NT_, CH = CH_, SEG = NT_ * CH_ * 16, WPE = WPE_;
 };
-using G_PROD = geom<1024, 8>;  // 128 KiB segments, 16 waves, one workgroup per CU (default)
-using G_PROD2 = geom<512, 8>;  // 64 KiB segments, 8 waves, two workgroups per CU (XYWS_OPT_WG512)
-using G_SMALL = geom<64, 1>;   // 1 KiB segments, one wave (XYWS_OPT_SMALL_SEG)
+using G_PROD = geom<1024, 8, 4>;  // 128 KiB segments, 16 waves, one workgroup per CU (default)
+using G_PROD2 = geom<512, 8, 4>;  // 64 KiB segments, 8 waves, two workgroups per CU (XYWS_OPT_WG512)
+using G_SMALL = geom<64, 1, 1>;   // 1 KiB segments, one wave (XYWS_OPT_SMALL_SEG)
 
 struct fent {
   uint32_t start, ps, end, kw;  // segment-relative, clamped to [0, 2^32-1]
 };
+// prologue lists (they overlay the frame list): candidates of one scan window
+// (u16 window offsets) and candidates whose chain left the segment (u32)
+constexpr uint32_t CCAP = FCAP * sizeof(fent) / 4, UCAP = FCAP * sizeof(fent) / 8;
 
 struct cstate {
   uint64_t X;          // next frame start (absolute)
@@ -116,7 +122,8 @@ struct run_params {
   uint64_t lo, hi;
   uint64_t nseg;          // segments covering [0, hi)
   uint32_t nruns, spr;    // runs, segments per run
-  const xyws_carry* cin;  // private snapshot of the incoming carry
+  const xyws_carry* cin_user;  // caller's incoming carry (nullable; may alias cout)
+  xyws_carry* cin;        // private snapshot of it, written by run 0 (finish/emit read it)
   xyws_carry* cout;
   xyws_frame* frames;
   uint64_t cap;
@@ -130,11 +137,17 @@ struct run_params {
 template <class G>
 struct __attribute__((aligned(16))) lds_t {
   uint8_t seg[G::SEG + PAD];
-  fent fl[FCAP];
+  union {
+    fent fl[FCAP];
+    struct {
+      uint16_t cl[CCAP];
+      uint32_t ul[UCAP];
+    };
+  };
   cstate S;
   cstate B;  // k_stream_finish: exact state handed to a repaired run
   uint64_t hn, Wn, succ, first_after, cnt, tail, aux0, aux1, aux2, bcnt, bfirst;
-  uint32_t nfl, pass_hi, known, past, ok, done, end, best, ticket, act, repaired;
+  uint32_t nfl, pass_hi, known, past, ok, done, end, best, ticket, act, repaired, ccnt, ucnt;
 };
 
 // ---------------------------------------------------------------- small helpers
@@ -149,7 +162,9 @@ XYWS_DEV uint32_t flag_load(const uint32_t* p) {
 }
 XYWS_DEV bool stats_on(const run_params& P) { return (P.opts & XYWS_OPT_STATS) != 0; }
 enum { ST_RUNS = 0, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRAMES,
-       ST_T_PRO = 16, ST_T_MAIN, ST_T_WAIT, ST_T_FILL, ST_T_CHASE, ST_T_XOR, ST_T_TAIL, ST_T_PF, ST_T_CP };
+       ST_P_WIN, ST_P_CAND, ST_P_UND, ST_P_TCOMP, ST_P_TCHECK, ST_P_TRES,
+       ST_T_PRO = 16, ST_T_MAIN, ST_T_WAIT, ST_T_FILL, ST_T_CHASE, ST_T_XOR, ST_T_TAIL, ST_T_PF, ST_T_CP,
+       ST_P_FILL, ST_P_SCAN, ST_P_PUB };
 XYWS_DEV void stat_add(const run_params& P, uint32_t i, uint64_t v) {
   if (stats_on(P)) atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + i, (unsigned long long)v);
 }
@@ -241,8 +256,7 @@ XYWS_DEV hdr_info hdr_at(const run_params& P, const lds_t<G>& L, uint64_t ss, ui
 
 // Header whose first h0 bytes were carried from the previous batch (the rest
 // from the batch start), assembled in registers.
-XYWS_DEV hdr_info header_carried(const run_params& P) {
-  const xyws_carry* c = P.cin;
+XYWS_DEV hdr_info header_carried(const run_params& P, const xyws_carry* c) {
   const uint32_t h0 = c->hdr_len < XYWS_MAX_FRAME_HEADER_SIZE ? c->hdr_len : XYWS_MAX_FRAME_HEADER_SIZE;
   uint32_t w[4] = {0u, 0u, 0u, 0u}, n = 0;
 #pragma unroll
@@ -284,11 +298,10 @@ XYWS_DEV uint32_t cand_nibble(uint32_t w, uint32_t wn, bool unmasked) {
 
 // State before the first byte of the batch, from the carry snapshot; cnt =
 // frames it completes (the carried-header frame).
-XYWS_DEV cstate initial_state(const run_params& P, uint64_t& cnt) {
+XYWS_DEV cstate initial_state(const run_params& P, const xyws_carry* c, uint64_t& cnt) {
   cstate s;
   s.X = P.lo; s.cov_ps = P.lo; s.cov_start = P.lo; s.cov_kw = 0; s.cov_key = 0; s.st = S_NOCOV; s.pad = 0;
   cnt = 0;
-  const xyws_carry* c = P.cin;
   const uint64_t R = c->payload_remaining;
   if (R) {
     const uint32_t k = (uint32_t)c->key[0] | ((uint32_t)c->key[1] << 8) |
@@ -300,7 +313,7 @@ XYWS_DEV cstate initial_state(const run_params& P, uint64_t& cnt) {
     return s;
   }
   if (c->hdr_len) {
-    const hdr_info h = header_carried(P);
+    const hdr_info h = header_carried(P, c);
     if (!h.hlen) {  // still incomplete: the whole batch belongs to the header
       s.st = S_NOCOV | S_PARTIAL | S_PARTCARRY;
       return s;
@@ -495,19 +508,28 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
       tm = t_;                                          \
     }                                                   \
   } while (0)
-  for (uint64_t s = s0;; s++) {
-    const uint64_t ss = s * G::SEG, nx = ss + G::SEG;
-    __syncthreads();  // the previous segment's LDS reads are done
-    XYWS_STAMP(acc_tail);
-    if (tid == 0 && !L.known && nx >= rng_end) {
-      // the next segment lies past the run's range: the write limit is the
-      // successor's W (its prologue published it long ago)
+  // Once the next segment lies past the run's range the write limit is the
+  // successor's W (its prologue published it long ago): looked up one
+  // iteration ahead, so that every prefetch decision is known before the fill.
+  auto lookup = [&](uint64_t nxt) {
+    if (tid == 0 && !L.known && nxt >= rng_end) {
       const uint64_t t0 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
       uint64_t hn, Wn, succ;
       lookup_successor(P, hn, Wn, succ, run);
       L.hn = hn; L.Wn = Wn; L.succ = succ; L.known = 1;
       if (stats_on(P)) stat_add(P, ST_T_WAIT, __builtin_amdgcn_s_memtime() - t0);
     }
+  };
+  lookup((s0 + 1) * G::SEG);
+  for (uint64_t s = s0;; s++) {
+    const uint64_t ss = s * G::SEG, nx = ss + G::SEG;
+    __syncthreads();  // the previous segment's LDS reads are done; L control words visible
+    XYWS_STAMP(acc_tail);
+    const bool known = L.known != 0;
+    const uint64_t wlim = known ? L.Wn : rng_end;
+    const uint64_t whi = wlim < P.hi ? wlim : P.hi;
+    const bool fin0 = (L.end || L.done) && nx >= whi;
+    const bool pf = nx < P.hi && nx < wlim && !fin0 && io.pf != s + 1;
     if (!(in_lds && s == s0)) {
 #pragma unroll
       for (uint32_t k = 0; k < G::CH; k++)
@@ -516,12 +538,9 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
     }
     __syncthreads();
     XYWS_STAMP(acc_fill);
-    const bool known = L.known != 0;
-    const uint64_t wlim = known ? L.Wn : rng_end;
-    const uint64_t whi = wlim < P.hi ? wlim : P.hi;
-    const bool fin0 = (L.end || L.done) && nx >= whi;
-    if (nx < P.hi && nx < wlim && !fin0 && io.pf != s + 1) io.issue(P, s + 1, tid);
-    XYWS_STAMP(acc_pf);
+    // (issuing each chunk's next load right after its LDS write made hipcc wait
+    // for the new loads inside the fill: the prefetch goes after the barrier)
+    if (pf) io.issue(P, s + 1, tid);
     const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, s);
     uint32_t lo_c = 0, keep = 0;
     for (;;) {
@@ -604,6 +623,7 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
     // continue while bytes below the write limit remain
     const bool fin = (L.end || L.done) && nx >= whi;
     if (nx >= P.hi || nx >= wlim || fin) break;
+    lookup(nx + G::SEG);
   }
   if (st_on && tid == 0) {
     stat_add(P, ST_T_TAIL, acc_tail);
@@ -621,22 +641,110 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
 // Earliest position of run `run`'s range whose chain of KHDR headers is
 // plausible (lane 0 returns it through L.aux0; NONE if there is none). Leaves
 // the segment it was found in (L.aux1) in LDS.
+// 0: implausible, 1: plausible, 2: undecided (only when !mem: the chain
+// leaves the segment held in LDS)
 template <class G>
-XYWS_DEV bool chain_plausible(const run_params& P, const lds_t<G>& L, uint64_t ss, uint64_t q, bool unm) {
+XYWS_DEV uint32_t chain_plausible(const run_params& P, const lds_t<G>& L, uint64_t ss, uint64_t q, bool unm,
+                                  bool mem) {
   uint64_t x = q;
   uint32_t need = KHDR_7;
   for (uint32_t i = 0; i < need; i++) {
     if (x >= P.hi) return i > 0;  // the chain ends with the batch
+    if (!mem && x - ss + XYWS_MAX_FRAME_HEADER_SIZE > G::SEG) return 2u;  // (x >= ss always)
     const hdr_info h = hdr_at(P, L, ss, x, NONE);
     if (!h.hlen) return i > 0;    // a header cut by the batch end
-    if (!plausible(h, unm)) return false;
+    if (!plausible(h, unm)) return 0u;
     if (i == 0) {
       const uint32_t ext = h.hlen - 2 - ((h.status & XYWS_ST_UNMASKED) ? 0u : 4u);
       need = ext == 8 ? KHDR_127 : ext == 2 ? KHDR_126 : KHDR_7;
     }
     x = sat_add(x + h.hlen, h.plen);
   }
-  return true;
+  return 1u;
+}
+
+// Candidate bits of the 16 positions of chunk a (bit t: position a + t).
+template <class G>
+XYWS_DEV uint32_t chunk_candidates(const run_params& P, const lds_t<G>& L, uint32_t a, bool unm) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(L.seg + a);
+  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+  uint32_t bits = cand_nibble(w0, w1, unm) | (cand_nibble(w1, w2, unm) << 4) |
+                  (cand_nibble(w2, w3, unm) << 8) | (cand_nibble(w3, w4, unm) << 12);
+  // headers straddling the segment end are left to the next segment's scan
+  if (a + 16 + 1 > G::SEG) bits &= (1u << (G::SEG - XYWS_MAX_FRAME_HEADER_SIZE - a + 1)) - 1u;
+  return bits;
+}
+
+// Prologue scan of the segment in LDS (see find_entry). mem = false: chains
+// leaving the segment are appended to L.ul (L.ucnt counts past UCAP on
+// overflow); mem = true: they are followed through memory.
+template <class G>
+XYWS_DEV void scan_windows(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid, bool unm, bool mem) {
+  const bool st_on = stats_on(P) && tid == 0;
+  uint64_t tq = st_on ? __builtin_amdgcn_s_memtime() : 0, a_comp = 0, a_check = 0, nwin = 0, ncand = 0;
+#pragma unroll 1
+  for (uint32_t k = 0; k < G::CH; k++) {
+    const uint32_t wb = k * G::NT * 16u;
+    if (ss + wb >= P.hi) break;
+    const uint32_t a = wb + tid * 16u;
+    const uint32_t bits = ss + a < P.hi ? chunk_candidates<G>(P, L, a, unm) : 0u;
+    if (tid == 0) L.ccnt = 0;
+    __syncthreads();
+    uint32_t tot = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < 16; t++) tot += __popcll(__ballot((bits >> t) & 1u));
+    uint32_t base = 0;
+    if ((tid & 63u) == 0 && tot) base = atomicAdd(&L.ccnt, tot);
+    base = __shfl(base, 0);
+#pragma unroll
+    for (uint32_t t = 0; t < 16; t++) {
+      const uint64_t m = __ballot((bits >> t) & 1u);
+      const uint32_t i = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (((bits >> t) & 1u) && i < CCAP) L.cl[i] = (uint16_t)(tid * 16u + t);
+      base += __popcll(m);
+    }
+    __syncthreads();
+    const uint32_t n = L.ccnt;
+    if (st_on) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      if (k == 0) stat_add(P, ST_P_TRES, t - tq);
+      a_comp += t - tq; tq = t; nwin++; ncand += n;
+    }
+    auto check = [&](uint32_t pos) {
+      const uint32_t v = chain_plausible(P, L, ss, ss + pos, unm, mem);
+      if (v == 1u) {
+        atomicMin(&L.best, pos);
+      } else if (v == 2u) {
+        const uint32_t u = atomicAdd(&L.ucnt, 1u);
+        if (u < UCAP) L.ul[u] = pos;
+      }
+      return v == 1u;
+    };
+    if (n <= CCAP) {
+      for (uint32_t i = tid; i < n; i += G::NT) {
+        const uint32_t pos = wb + L.cl[i];
+        if (pos < __hip_atomic_load(&L.best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) check(pos);
+      }
+    } else {  // more candidates than the list holds: each lane checks its own
+      uint32_t b = bits;
+      while (b) {
+        const uint32_t t = __builtin_ctz(b);
+        b &= b - 1;
+        if (check(a + t)) break;
+      }
+    }
+    __syncthreads();
+    if (st_on) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      a_check += t - tq; tq = t;
+    }
+    if (L.best != 0xFFFFFFFFu) break;
+  }
+  if (st_on) {
+    stat_add(P, ST_P_WIN, nwin); stat_add(P, ST_P_CAND, ncand);
+    stat_add(P, ST_P_TCOMP, a_comp); stat_add(P, ST_P_TCHECK, a_check);
+  }
 }
 
 template <class G>
@@ -646,41 +754,47 @@ XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32
   uint64_t s_end = s_begin + P.spr;
   if (s_end > P.nseg) s_end = P.nseg;
   if (tid == 0) L.aux0 = NONE;
+  uint64_t tp = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
   for (uint64_t s = s_begin; s < s_end; s++) {
     const uint64_t ss = s * G::SEG;
     __syncthreads();
     io.fill(P, L, s, tid);
     if (tid == 0) { L.best = 0xFFFFFFFFu; L.aux1 = s; }
     __syncthreads();
-    if (s + 1 < P.nseg) io.issue(P, s + 1, tid);
-    bool found = false;
-#pragma unroll 1
-    for (uint32_t k = 0; k < G::CH && !found; k++) {
-      const uint32_t a = (k * G::NT + tid) * 16u;
-      const uint64_t A = ss + a;
-      if (A >= P.hi) break;
-      const uint32_t* q = reinterpret_cast<const uint32_t*>(L.seg + a);
-      const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
-      uint32_t bits = cand_nibble(w0, w1, unm) | (cand_nibble(w1, w2, unm) << 4) |
-                      (cand_nibble(w2, w3, unm) << 8) | (cand_nibble(w3, w4, unm) << 12);
-      // headers straddling the segment end are left to the next segment's scan
-      if (a + 16 + 1 > G::SEG) bits &= (1u << (G::SEG - XYWS_MAX_FRAME_HEADER_SIZE - a + 1)) - 1u;
-      while (bits) {
-        const uint32_t t = __builtin_ctz(bits);
-        bits &= bits - 1;
-        const uint32_t pos = a + t;
-        if (pos > __hip_atomic_load(&L.best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-          found = true;
-          break;
-        }
-        if (chain_plausible(P, L, ss, ss + pos, unm)) {
-          atomicMin(&L.best, pos);
-          found = true;
-          break;
-        }
+    if (stats_on(P) && tid == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      stat_add(P, ST_P_FILL, t - tp);
+      tp = t;
+    }
+    // (no prefetch during the scan: a header read from memory, and the
+    // publish's vmcnt(0), would wait for it)
+    // One window of NT chunks (16 B per thread, contiguous) at a time: the
+    // window's candidates are compacted into an LDS list and their chains are
+    // checked one candidate per lane (a per-thread loop would make every wave
+    // wait for its lane with the most candidates); the earliest plausible one
+    // wins, and windows are in position order, so the first window with a
+    // winner ends the scan. Chains are followed in LDS only; candidates whose
+    // chain leaves the segment are listed and resolved from memory afterwards,
+    // all at once (one memory latency for the scan, not one per window).
+    if (tid == 0) L.ucnt = 0;
+    scan_windows<G>(P, L, ss, tid, unm, false);
+    const uint32_t nu = L.ucnt;
+    if (stats_on(P) && tid == 0) stat_add(P, ST_P_UND, nu);
+    if (nu > UCAP) {  // the list overflowed: scan again following chains through memory
+      scan_windows<G>(P, L, ss, tid, unm, true);
+    } else if (nu) {
+      const uint32_t best = L.best;
+      for (uint32_t i = tid; i < nu; i += G::NT) {
+        const uint32_t pos = L.ul[i];
+        if (pos < best && chain_plausible(P, L, ss, ss + pos, unm, true) == 1u) atomicMin(&L.best, pos);
       }
     }
     __syncthreads();
+    if (stats_on(P) && tid == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      stat_add(P, ST_P_SCAN, t - tp);
+      tp = t;
+    }
     if (L.best != 0xFFFFFFFFu) {
       if (tid == 0) L.aux0 = ss + L.best;
       break;
@@ -691,7 +805,7 @@ XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32
 
 // ---------------------------------------------------------------- kernels
 template <class G>
-__global__ void __launch_bounds__(G::NT) k_stream_runs(run_params P) {
+__global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
   lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
   const uint32_t tid = threadIdx.x;
@@ -708,8 +822,17 @@ __global__ void __launch_bounds__(G::NT) k_stream_runs(run_params P) {
   bool in_lds = false;
   if (run == 0) {
     if (tid == 0) {
+      // snapshot of the incoming carry for k_stream_finish / k_stream_emit
+      // (the caller's carry may alias the carry out, which finish writes)
+      xyws_carry cz;
+      if (P.cin_user) {
+        cz = *P.cin_user;
+      } else {
+        for (int i = 0; i < 64; i++) reinterpret_cast<uint8_t*>(&cz)[i] = 0;
+      }
+      *P.cin = cz;
       uint64_t c0;
-      L.S = initial_state(P, c0);
+      L.S = initial_state(P, &cz, c0);
       L.cnt = c0;
       st_store(rec + R_H, P.lo);
       st_store(rec + R_W, P.lo);
@@ -720,6 +843,7 @@ __global__ void __launch_bounds__(G::NT) k_stream_runs(run_params P) {
     s0 = 0;
   } else {
     find_entry(P, L, io, tid, run);
+    const uint64_t tpub = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
     if (tid == 0) {
       const uint64_t q = L.aux0, seg_q = L.aux1;
       const uint64_t ss = seg_q * G::SEG;
@@ -757,12 +881,15 @@ __global__ void __launch_bounds__(G::NT) k_stream_runs(run_params P) {
       stat_add(P, ST_RUNS, 1);
       if (h == NONE) stat_add(P, ST_NONE, 1);
       if (stats_on(P)) stat_add(P, ST_T_PRO, __builtin_amdgcn_s_memtime() - t0);
+      if (stats_on(P)) stat_add(P, ST_P_PUB, __builtin_amdgcn_s_memtime() - tpub);
     }
     __syncthreads();
     if (L.aux2 == NONE) return;  // no entry: the chain of an earlier run covers this range
     wlo = L.aux2;
     s0 = wlo / G::SEG;
     in_lds = s0 == L.aux1;
+    // published: now the next segment's loads
+    if (in_lds && (s0 + 1) * G::SEG < P.hi) io.issue(P, s0 + 1, tid);
   }
   if (tid == 0) {
     L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.first_after = NONE;
@@ -941,7 +1068,11 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
     __syncthreads();
   }
   }  // serial walk with repairs
+  // every run has exited: the ticket and the prologue flags start the next
+  // call at zero (no per-call memset; scratch is zeroed when allocated)
+  for (uint32_t r = tid; r < P.nruns; r += G::NT) P.flags[r] = 0;
   if (tid == 0) {
+    P.head[0] = 0;
     const uint64_t total = L.aux2;
     const cstate o = L.S;
     if (P.nframes) *P.nframes = total;
@@ -967,7 +1098,7 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
           c.phase = P.cin->phase + (hi - lo);
           for (int i = 0; i < 4; i++) c.key[i] = P.cin->key[i];
         } else {
-          const hdr_info hh = (o.st & S_HDRCARRY) ? header_carried(P) : hdr_global(P, o.cov_start, NONE);
+          const hdr_info hh = (o.st & S_HDRCARRY) ? header_carried(P, P.cin) : hdr_global(P, o.cov_start, NONE);
           c.payload_remaining = hh.plen - (hi - o.cov_ps);
           c.phase = hi - o.cov_ps;
           c.key[0] = (uint8_t)hh.key; c.key[1] = (uint8_t)(hh.key >> 8);
@@ -1008,7 +1139,7 @@ __global__ void __launch_bounds__(64) k_stream_emit(run_params P) {
   if (st_load(rec + R_ECARRY)) {  // run 0: the carried-header frame comes first
     X = P.lo;
     if (!P.cin->payload_remaining && P.cin->hdr_len) {
-      const hdr_info hh = header_carried(P);
+      const hdr_info hh = header_carried(P, P.cin);
       if (hh.hlen) {
         const uint64_t ps = P.lo + (hh.hlen - P.cin->hdr_len);
         write_frame(P, ord++, P.lo, hh, ps, (int32_t)P.cin->hdr_len);
@@ -1093,7 +1224,7 @@ static int scratch_grow(stream_scratch* s, uint64_t runs) {
   s->mem = m;
   s->bytes = bytes;
   s->max_runs = want;
-  return hipMemset(m, 0, HEAD_BYTES) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
+  return hipMemset(m, 0, HEAD_BYTES + flags_bytes(want)) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
 
 int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
@@ -1154,19 +1285,12 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   P.flags = reinterpret_cast<uint32_t*>(m + HEAD_BYTES);
   P.rec = reinterpret_cast<uint64_t*>(m + HEAD_BYTES + flags_bytes(s->max_runs));
   P.opts = opts;
-  // Ticket and total zeroed every call (the error word [1] is sticky until read
-  // back). The carry is snapshotted first: dev_carry_in may alias dev_carry_out.
-  xyws_carry* snap = reinterpret_cast<xyws_carry*>(m + 64);
-  if (hipMemsetAsync(P.head, 0, 4, stream) != hipSuccess) return XYWS_ERR_HIP;
+  // The ticket and the flags are zero here (zeroed at allocation, reset by
+  // k_stream_finish after every call); the error word [1] is sticky until read
+  // back. Run 0 snapshots the incoming carry into scratch.
   if ((opts & XYWS_OPT_STATS) && hipMemsetAsync(m + 128, 0, 256, stream) != hipSuccess) return XYWS_ERR_HIP;
-  if (cin) {
-    if (hipMemcpyAsync(snap, cin, sizeof(xyws_carry), hipMemcpyDeviceToDevice, stream) != hipSuccess)
-      return XYWS_ERR_HIP;
-  } else if (hipMemsetAsync(snap, 0, sizeof(xyws_carry), stream) != hipSuccess) {
-    return XYWS_ERR_HIP;
-  }
-  P.cin = snap;
-  if (hipMemsetAsync(P.flags, 0, (4 * nruns + 15) & ~15ull, stream) != hipSuccess) return XYWS_ERR_HIP;
+  P.cin_user = cin;
+  P.cin = reinterpret_cast<xyws_carry*>(m + 64);
   return small ? launch_runs<G_SMALL>(P, stream)
                : wg512 ? launch_runs<G_PROD2>(P, stream) : launch_runs<G_PROD>(P, stream);
 }
