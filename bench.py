@@ -264,8 +264,8 @@ def main():
 
     if args.stats and rank == 0:  # one extra counted decode pair (keeps the step parity)
         names = ["runs", "runs_without_entry", "bad_boundaries", "repairs", "cuts", "spins", "segments",
-                 "frames", "scan_windows", "scan_candidates", "scan_undecided", "cyc_scan_compact",
-                 "cyc_scan_check", "cyc_scan_comp_first", "-", "-", "cyc_prologue", "cyc_main", "cyc_wait",
+                 "frames", "scan_segments", "scan_survivors", "scan_undecided", "cyc_scan_filter",
+                 "cyc_scan_check", "cyc_scan_resolve", "-", "-", "cyc_prologue", "cyc_main", "cyc_wait",
                  "cyc_fill", "cyc_chase_sync", "cyc_xor", "cyc_tail", "cyc_prefetch_issue", "cyc_chase_pass",
                  "cyc_pro_fill", "cyc_pro_scan", "cyc_pro_publish"]
         for _ in range(2):

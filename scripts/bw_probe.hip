@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(NT) k_runs_buf(u32x4* p, uint64_t bytes, uint3
 // 7. 1024-thread runs, SEGB per iteration, nt buffer ops, LDS copy of the
 //    current segment for header access. XFROM_LDS: XOR source is the LDS copy
 //    (else a register copy kept alongside).
-template <int NT, int SEGB, bool XFROM_LDS>
+template <int NT, int SEGB, bool XFROM_LDS, int WALK = 3, int XOPS = 0>
 __global__ void __launch_bounds__(NT) k_runs_lds2(u32x4* p, uint64_t bytes, uint32_t kw) {
   constexpr int CH = SEGB / 16 / NT;
   extern __shared__ __attribute__((aligned(16))) u32x4 lds2[];
@@ -189,13 +189,17 @@ __global__ void __launch_bounds__(NT) k_runs_lds2(u32x4* p, uint64_t bytes, uint
     }
     if (threadIdx.x == 0) {  // dependent LDS walk (stand-in for the chase)
       uint32_t x = 0;
-      for (int h = 0; h < 3; h++) x = lds2[(x + 17) & (SEGB / 16 - 1)].x & (SEGB / 16 - 1);
+      for (int h = 0; h < WALK; h++) x = lds2[(x + 17) & (SEGB / 16 - 1)].x & (SEGB / 16 - 1);
       if (x == 0xFFFFFFFF) lds2[0].w = 0;
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < CH; k++) {
       u32x4 v = XFROM_LDS ? lds2[k * NT + threadIdx.x] : c[k];
+      uint32_t kk = kw;
+#pragma unroll
+      for (int o = 0; o < XOPS; o++) kk = __builtin_amdgcn_alignbyte(kk, v.x, o & 3) ^ (kk >> 1);
+      if (XOPS) v.y ^= kk & 0x80000000u;
       __builtin_amdgcn_raw_buffer_store_b128(v ^ kw, rs, vo, (uint32_t)((s - s0) * SEGB + k * NT * 16), 2);
     }
   }
@@ -230,6 +234,11 @@ int main(int argc, char** argv) {
   CK(hipFuncSetAttribute((const void*)k_runs_lds2<1024, 131072, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
   CK(hipFuncSetAttribute((const void*)k_runs_lds2<1024, 131072, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
   run("lds2 1024t 128K fromLDS x1", [&] { k_runs_lds2<1024, 131072, true><<<ncu, 1024, 131072>>>(p, bytes, 0x1234567u); });
+#define WV(W, X) \
+  CK(hipFuncSetAttribute((const void*)k_runs_lds2<1024, 131072, true, W, X>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072)); \
+  run("lds2 128K walk " #W " xops " #X, [&] { k_runs_lds2<1024, 131072, true, W, X><<<ncu, 1024, 131072>>>(p, bytes, 0x1234567u); });
+  WV(30, 0) WV(100, 0) WV(300, 0) WV(3, 16) WV(3, 48) WV(3, 96) WV(100, 48)
+  if (argc > 1) return 0;
   run("lds2 1024t 128K fromREG x1", [&] { k_runs_lds2<1024, 131072, false><<<ncu, 1024, 131072>>>(p, bytes, 0x1234567u); });
   run("lds2 1024t 64K fromLDS x2", [&] { k_runs_lds2<1024, 65536, true><<<ncu * 2, 1024, 65536>>>(p, bytes, 0x1234567u); });
   run("lds2 512t 64K fromLDS x2", [&] { k_runs_lds2<512, 65536, true><<<ncu * 2, 512, 65536>>>(p, bytes, 0x1234567u); });

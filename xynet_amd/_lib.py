@@ -83,6 +83,8 @@ def load():
     L.xyws_decode_indexed.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp]
     L.xyws_debug_stats.restype = i32
     L.xyws_debug_stats.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.xyws_debug_records.restype = C.c_int64
+    L.xyws_debug_records.argtypes = [vp, C.POINTER(C.c_uint64), u64]
     L.xyws_decode_stream.restype = i32
     L.xyws_decode_stream.argtypes = [vp, vp, u64, vp, vp, vp, u64, vp, u32, vp]
     _lib = L

@@ -422,6 +422,15 @@ int xyws_debug_stats(xyws_ctx* ctx, uint64_t out[32]) {
   return stream_scratch_stats(&ctx->ss, out);
 }
 
+// Internal: the run records of the last fused stream decode (24 u64 per run,
+// layout in xyws_stream.hip), at most max_runs of them; returns the count
+// copied or a negative error. Synchronizes the device.
+int64_t xyws_debug_records(xyws_ctx* ctx, uint64_t* out, uint64_t max_runs) {
+  if (!ctx || !out) return XYWS_ERR_INVALID;
+  device_guard g(ctx->device);
+  return stream_scratch_records(&ctx->ss, out, max_runs);
+}
+
 int xyws_unmask(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4], uint64_t phase,
                 uint64_t* phase_out, void* stream) {
   if (!ctx || !key || (!dev && len)) return XYWS_ERR_INVALID;

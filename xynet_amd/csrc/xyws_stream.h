@@ -18,6 +18,7 @@ void stream_scratch_free(stream_scratch* s);
 int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes);
 uint32_t stream_scratch_error(stream_scratch* s);
 int stream_scratch_stats(stream_scratch* s, uint64_t out[32]);
+int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_runs);
 
 // Internal decode options (not part of include/xyws.h):
 #define XYWS_OPT_STATS 0x100u      // count speculation/repair events (xyws_debug_stats)
@@ -25,6 +26,7 @@ int stream_scratch_stats(stream_scratch* s, uint64_t out[32]);
                                    // speculation and repair on small test inputs
 #define XYWS_OPT_NO_STORE 0x20000u // diagnostics: decode without writing (timing split only)
 #define XYWS_OPT_WG512 0x40000u    // two 512-thread workgroups per CU, 64 KiB segments
+#define XYWS_OPT_DIAG 0x80000u     // diagnostics: no prefetch during the prologue scan (timing only)
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
                         const xyws_carry* cin, xyws_carry* cout, xyws_frame* frames, uint64_t cap,
                         uint64_t* nframes, uint32_t opts, hipStream_t stream);

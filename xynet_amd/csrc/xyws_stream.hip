@@ -13,7 +13,7 @@
 // 16-byte buffer loads/stores and a one-segment register prefetch. This kernel
 // is that data movement plus the header chase:
 //
-//  * The batch is cut into RUNS of whole segments, one per workgroup (a ticket
+//  * The batch is cut into RUNS of equal byte ranges, one per workgroup (a ticket
 //    gives runs out in dispatch order).
 //  * Inside a run the chase is EXACT and serial: lane 0 parses each header from
 //    the LDS copy of the segment and appends (payload range, rotated key word) to
@@ -62,10 +62,15 @@ constexpr uint32_t FCAP = 512;        // frame-list entries per pass
 constexpr uint32_t PAD = 32;          // LDS bytes after the segment (5-dword header reads)
 // Headers a speculative entry's chain must pass, by the entry's length form:
 // a false 127-form header needs 0xFF/0x7F plus an 8-byte length below 2^46
-// (~5e-10 per random position), a 126-form one 0xFE/0x7E (~1.4e-4), a 7-bit
-// one just a plausible first byte (~1.7e-2); each further plausible header
-// multiplies by ~1.8e-2. Short hops mostly stay in LDS; long ones are memory reads.
-constexpr uint32_t KHDR_127 = 1, KHDR_126 = 4, KHDR_7 = 6;
+// (~3e-10 per random position), a 126-form one 0xFE/0x7E (~9e-5), a 7-bit
+// one a plausible first byte and mask bit (~2.3e-2); each further plausible
+// header multiplies by ~2.3e-2. A prologue scans up to a few MB of payload
+// when frames are large (2^28 positions per call over all runs at 1 MiB
+// frames), so a false chain costs ~1e-12 per position (127 form: ~8e-12, two
+// headers, the second one mostly still in LDS for 64 KiB frames): ~1e-3 per
+// call at worst. Short hops stay in LDS; long ones are memory reads (batched
+// after the scan). A false entry costs time (a repair), never bytes.
+constexpr uint32_t KHDR_127 = 2, KHDR_126 = 6, KHDR_7 = 8;
 constexpr uint32_t SPIN = 1u << 24;   // bounded spins (s_sleep 2 each: ~1 s)
 constexpr uint32_t OOB = 0x80000000u; // buffer offset past every range: load 0, store dropped
 constexpr int AUX_NT = 2;             // buffer cache policy: nontemporal
@@ -94,9 +99,9 @@ using G_SMALL = geom<64, 1, 1>;   // 1 KiB segments, one wave (XYWS_OPT_SMALL_SE
 struct fent {
   uint32_t start, ps, end, kw;  // segment-relative, clamped to [0, 2^32-1]
 };
-// prologue lists (they overlay the frame list): candidates of one scan window
-// (u16 window offsets) and candidates whose chain left the segment (u32)
-constexpr uint32_t CCAP = FCAP * sizeof(fent) / 4, UCAP = FCAP * sizeof(fent) / 8;
+// prologue lists (they overlay the frame list): survivors of a segment's scan
+// filter and survivors whose chain left the segment (u32 segment offsets)
+constexpr uint32_t SCAP = FCAP * sizeof(fent) / 8, UCAP = FCAP * sizeof(fent) / 8;
 
 struct cstate {
   uint64_t X;          // next frame start (absolute)
@@ -120,8 +125,8 @@ enum {
 struct run_params {
   uint8_t* base;
   uint64_t lo, hi;
-  uint64_t nseg;          // segments covering [0, hi)
-  uint32_t nruns, spr;    // runs, segments per run
+  uint64_t rbytes;        // bytes per run range (multiple of 16); run r: [r*rbytes, (r+1)*rbytes)
+  uint32_t nruns;
   const xyws_carry* cin_user;  // caller's incoming carry (nullable; may alias cout)
   xyws_carry* cin;        // private snapshot of it, written by run 0 (finish/emit read it)
   xyws_carry* cout;
@@ -140,14 +145,19 @@ struct __attribute__((aligned(16))) lds_t {
   union {
     fent fl[FCAP];
     struct {
-      uint16_t cl[CCAP];
+      uint32_t sl[SCAP];
       uint32_t ul[UCAP];
     };
   };
   cstate S;
   cstate B;  // k_stream_finish: exact state handed to a repaired run
   uint64_t hn, Wn, succ, first_after, cnt, tail, aux0, aux1, aux2, bcnt, bfirst;
-  uint32_t nfl, pass_hi, known, past, ok, done, end, best, ticket, act, repaired, ccnt, ucnt;
+  uint32_t nfl, pass_hi, known, past, ok, done, end, best, ticket, act, repaired, ccnt, ucnt, keepn;
+  // per 1 KiB row of the segment (one wave-instruction of chunks), set by
+  // wave 0 after each chase pass: ROW_FAST (one key word for the whole row,
+  // rk), ROW_SKIP (nothing to store) or the entry to start the walk from
+  uint32_t rt[G::SEG / 1024];
+  uint32_t rk[G::SEG / 1024];
 };
 
 // ---------------------------------------------------------------- small helpers
@@ -330,9 +340,11 @@ XYWS_DEV cstate initial_state(const run_params& P, const xyws_carry* c, uint64_t
 
 // ---------------------------------------------------------------- segment I/O
 template <class G>
-XYWS_DEV __amdgpu_buffer_rsrc_t seg_rsrc(const run_params& P, uint64_t s) {
-  // [ss, ss + min(SEG, round16(hi) - ss)): loads past the batch read zero
-  const uint64_t ss = s * G::SEG, top = (P.hi + 15) & ~15ull;
+XYWS_DEV __amdgpu_buffer_rsrc_t seg_rsrc(const run_params& P, uint64_t ss, uint64_t lim = NONE) {
+  // [ss, ss + min(SEG, top - ss)), top = min(round16(hi), lim): loads past it
+  // read zero without touching memory
+  uint64_t top = (P.hi + 15) & ~15ull;
+  if (lim < top) top = (lim + 15) & ~15ull;
   const uint64_t room = top > ss ? top - ss : 0;
   const uint32_t n = room >= G::SEG ? G::SEG : (uint32_t)room;
   return __builtin_amdgcn_make_buffer_rsrc(P.base + ss, 0, n, 0x00020000);
@@ -341,17 +353,18 @@ XYWS_DEV __amdgpu_buffer_rsrc_t seg_rsrc(const run_params& P, uint64_t s) {
 template <class G>
 struct seg_io {
   u32x4 e[G::CH];
-  uint64_t pf = NONE;  // segment whose loads are in e
-  XYWS_DEV void issue(const run_params& P, uint64_t s, uint32_t tid) {
-    const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, s);
+  uint64_t pf = NONE;  // start of the segment whose loads are in e
+  // loads of the segment at ss (bytes at or past lim are not needed: zero)
+  XYWS_DEV void issue(const run_params& P, uint64_t ss, uint32_t tid, uint64_t lim = NONE) {
+    const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss, lim);
 #pragma unroll
     for (uint32_t k = 0; k < G::CH; k++)
       e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16u, k * G::NT * 16u, AUX_NT);
-    pf = s;
+    pf = ss;
   }
-  // segment s into LDS (caller syncs before and after)
-  XYWS_DEV void fill(const run_params& P, lds_t<G>& L, uint64_t s, uint32_t tid) {
-    if (pf != s) issue(P, s, tid);
+  // the segment at ss into LDS (caller syncs before and after)
+  XYWS_DEV void fill(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid) {
+    if (pf != ss) issue(P, ss, tid);
 #pragma unroll
     for (uint32_t k = 0; k < G::CH; k++)
       *reinterpret_cast<u32x4*>(&L.seg[(k * G::NT + tid) * 16u]) = e[k];
@@ -446,6 +459,37 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   L.pass_hi = seg_done ? G::SEG : (uint32_t)((S.X - ss) & ~15ull);
 }
 
+// Row table of one pass (wave 0, after lane 0's chase_pass; rows r = lane,
+// lane + 64, ...): a row [r*1024, r*1024 + 1024) is FAST when every chunk in it
+// is stored whole with the key word of one entry, SKIP when no chunk in it is
+// stored, else the walk of its chunks starts at the last entry starting at or
+// before the row (binary search).
+constexpr uint32_t ROW_FAST = 1u << 16, ROW_SKIP = 1u << 17;
+template <class G>
+XYWS_DEV void build_rows(lds_t<G>& L, uint32_t nfl, uint32_t lo_c, uint32_t hi_c, uint32_t wl_r,
+                         uint32_t wh_r, bool any, uint32_t lane) {
+  for (uint32_t r = lane; r < G::SEG / 1024; r += 64) {
+    const uint32_t R0 = r * 1024, R1 = R0 + 1024;
+    uint32_t info = ROW_SKIP, kw = 0;
+    if (any && nfl && R1 > lo_c && R0 < hi_c && R1 > wl_r && R0 < wh_r) {
+      uint32_t x = 0, y = nfl;
+      while (y - x > 1) {
+        const uint32_t mid = (x + y) >> 1;
+        if (L.fl[mid].start <= R0) x = mid; else y = mid;
+      }
+      const fent e = L.fl[x];
+      const uint32_t ns = x + 1 < nfl ? L.fl[x + 1].start : 0xFFFFFFFFu;
+      info = x;
+      if (R0 >= lo_c && R1 <= hi_c && R0 >= wl_r && R1 <= wh_r && e.ps <= R0 && e.end >= R1 && ns >= R1) {
+        info = e.kw ? ROW_FAST : ROW_SKIP;
+        kw = e.kw;
+      }
+    }
+    L.rt[r] = info;
+    L.rk[r] = kw;
+  }
+}
+
 // The next run after `run` that has an entry (lane 0). Waits for each
 // candidate's prologue; every one of them took its ticket after ours.
 XYWS_DEV void lookup_successor(const run_params& P, uint64_t& hn, uint64_t& Wn, uint64_t& succ, uint32_t run) {
@@ -472,12 +516,12 @@ XYWS_DEV void lookup_successor(const run_params& P, uint64_t& hn, uint64_t& Wn, 
 }
 
 // Apply the chain in L.S (set by lane 0 together with L.known/hn/Wn/succ and
-// zeroed counters) from segment s0: every byte in [wlo, write limit) is XORed
+// zeroed counters) from the segment at ss0: every byte in [wlo, write limit) is XORed
 // with the key of the frame covering it, the write limit being the successor's
 // W (looked up before the first segment at or past rng_end, unless known). The
 // chase stops at the successor's W; L.ok tells whether it landed on its entry.
 template <class G>
-XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint64_t s0,
+XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint64_t ss0,
                         bool in_lds, uint64_t wlo, uint64_t rng_end, uint32_t run) {
   const bool stores = (P.opts & XYWS_OPT_PARSE_ONLY) == 0;
   const uint64_t wl = wlo > P.lo ? wlo : P.lo;
@@ -486,15 +530,15 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
   // issues exactly CH stores per lane (skipped chunks go to an out-of-range
   // offset), so each fill waits for its loads only (vmcnt counts loads and
   // stores together, in issue order) while the previous segment's stores drain.
-  if (!in_lds && io.pf != s0) io.issue(P, s0, tid);
+  if (!in_lds && io.pf != ss0) io.issue(P, ss0, tid, L.known ? L.Wn : NONE);
   {
     // CH dropped stores (out-of-range offset: no memory traffic) so that on
     // every path into the loop at least CH stores are younger than the loads:
     // the compiler's wait before the fill is then vmcnt(CH), not vmcnt(0)
-    const __amdgpu_buffer_rsrc_t rz = seg_rsrc<G>(P, s0);
+    const __amdgpu_buffer_rsrc_t rz = seg_rsrc<G>(P, ss0);
 #pragma unroll
     for (uint32_t k = 0; k < G::CH; k++)
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rz, OOB, 0, AUX_NT);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rz, OOB, k * G::NT * 16u, AUX_NT);  // distinct: not merged
   }
   // stats builds: wave 0 accumulates phase cycles in registers, flushed once
   const bool st_on = stats_on(P) && tid < 64;
@@ -520,17 +564,17 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
       if (stats_on(P)) stat_add(P, ST_T_WAIT, __builtin_amdgcn_s_memtime() - t0);
     }
   };
-  lookup((s0 + 1) * G::SEG);
-  for (uint64_t s = s0;; s++) {
-    const uint64_t ss = s * G::SEG, nx = ss + G::SEG;
+  lookup(ss0 + G::SEG);
+  for (uint64_t ss = ss0;; ss += G::SEG) {
+    const uint64_t nx = ss + G::SEG;
     __syncthreads();  // the previous segment's LDS reads are done; L control words visible
     XYWS_STAMP(acc_tail);
     const bool known = L.known != 0;
     const uint64_t wlim = known ? L.Wn : rng_end;
     const uint64_t whi = wlim < P.hi ? wlim : P.hi;
     const bool fin0 = (L.end || L.done) && nx >= whi;
-    const bool pf = nx < P.hi && nx < wlim && !fin0 && io.pf != s + 1;
-    if (!(in_lds && s == s0)) {
+    const bool pf = nx < P.hi && nx < wlim && !fin0 && io.pf != nx;
+    if (!(in_lds && ss == ss0)) {
 #pragma unroll
       for (uint32_t k = 0; k < G::CH; k++)
         *reinterpret_cast<u32x4*>(&L.seg[(k * G::NT + tid) * 16u]) = io.e[k];
@@ -540,67 +584,107 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
     XYWS_STAMP(acc_fill);
     // (issuing each chunk's next load right after its LDS write made hipcc wait
     // for the new loads inside the fill: the prefetch goes after the barrier)
-    if (pf) io.issue(P, s + 1, tid);
-    const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, s);
+    if (pf) io.issue(P, nx, tid, known ? wlim : NONE);
+    const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss);
     uint32_t lo_c = 0, keep = 0;
     for (;;) {
-      if (tid == 0) chase_pass(P, L, ss, lo_c, keep);
+      // write window [wl, whi) relative to the segment (32-bit compares below)
+      const uint32_t wl_r = wl > ss ? (wl - ss < G::SEG ? (uint32_t)(wl - ss) : G::SEG) : 0u;
+      const uint32_t wh_r = whi > ss ? (whi - ss < G::SEG ? (uint32_t)(whi - ss) : G::SEG) : 0u;
+      const bool any = stores && !(P.opts & XYWS_OPT_NO_STORE) && wl_r < wh_r;
+      if (tid < 64) {
+        // lane 0 chases; then wave 0 classifies the rows (the other waves wait
+        // at the barrier with their prefetch in flight: work here is hidden,
+        // work in the store loop below is not)
+        if (tid == 0) chase_pass(P, L, ss, lo_c, keep);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        build_rows<G>(L, L.nfl, lo_c, L.pass_hi, wl_r, wh_r, any, tid);
+      }
       XYWS_STAMP(acc_cp);
       __syncthreads();
       XYWS_STAMP(acc_sync);
       const uint32_t nfl = L.nfl, hi_c = L.pass_hi;
-      // each lane walks the sorted, contiguous frame list once, forward with
-      // its chunks: entry g covers the chunk when no later entry starts in it
-      // and its payload spans it (the common case: one key word for all four
-      // dwords); chunks holding a header or a frame boundary take chunk_xor
-      // write window [wl, whi) relative to the segment (32-bit compares below)
-      const uint32_t wl_r = wl > ss ? (wl - ss < G::SEG ? (uint32_t)(wl - ss) : G::SEG) : 0u;
-      const uint32_t wh_r = whi > ss ? (whi - ss < G::SEG ? (uint32_t)(whi - ss) : G::SEG) : 0u;
-      const bool any = stores && nfl && wl_r < wh_r;
-      uint32_t g = 0, edge = 0;
-      fent e = L.fl[0];
-      uint32_t ns = nfl > 1 ? L.fl[1].start : 0xFFFFFFFFu;
+      // Per chunk: a FAST row XORs with one scalar key word, a SKIP row stores
+      // nothing; otherwise the lane walks the sorted, contiguous frame list from
+      // the row's entry: entry g covers the chunk when no later entry starts in
+      // it and its payload spans it (one key word for all four dwords). Every
+      // chunk issues exactly one store here (dropped ones to the out-of-range
+      // offset); chunks holding a header or a frame boundary, and the batch's
+      // first/last chunk, are left to the loop after it (few registers live in
+      // this unrolled loop: the next segment's loads are in flight).
+      uint32_t edge = 0;
+      const uint32_t wave = tid >> 6;
 #pragma unroll
       for (uint32_t k = 0; k < G::CH; k++) {
         const uint32_t a = (k * G::NT + tid) * 16u;
-        const bool in = any && a >= lo_c && a < hi_c && a + 16 > wl_r && a < wh_r;
-        u32x4 m = {0u, 0u, 0u, 0u};
-        if (in) {
-          while (ns <= a) {
-            g++;
-            e = L.fl[g];
-            ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
-          }
-          if (e.ps <= a && e.end >= a + 16 && ns >= a + 16) m = u32x4{e.kw, e.kw, e.kw, e.kw};
-          else m = chunk_xor(L, nfl, g, a);
-        }
-        const bool nz = (m.x | m.y | m.z | m.w) != 0u;
-        const bool full = a >= wl_r && a + 16 <= wh_r;
+        const uint32_t row = k * (G::NT / 64) + wave;
+        const uint32_t info = __builtin_amdgcn_readfirstlane(L.rt[row]);
         const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
-        __builtin_amdgcn_raw_buffer_store_b128(v ^ m, rs,
-                                               (in && nz && full && !(P.opts & XYWS_OPT_NO_STORE)) ? tid * 16u : OOB,
-                                               k * G::NT * 16u, AUX_NT);
+        u32x4 m;
+        uint32_t off;
+        if (info & ROW_FAST) {
+          const uint32_t kw = __builtin_amdgcn_readfirstlane(L.rk[row]);
+          m = u32x4{kw, kw, kw, kw};
+          off = tid * 16u;
+        } else if (info & ROW_SKIP) {
+          m = u32x4{0u, 0u, 0u, 0u};
+          off = OOB;
+        } else {
+          const bool in = a >= lo_c && a < hi_c && a + 16 > wl_r && a < wh_r;
+          m = u32x4{0u, 0u, 0u, 0u};
+          off = OOB;
+          if (in) {
+            uint32_t g = info;
+            fent e = L.fl[g];
+            uint32_t ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
+            while (ns <= a) {
+              g++;
+              e = L.fl[g];
+              ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
+            }
+            const bool simple = e.ps <= a && e.end >= a + 16 && ns >= a + 16;
+            const bool full = a >= wl_r && a + 16 <= wh_r;
+            if (simple && full) {
+              m = u32x4{e.kw, e.kw, e.kw, e.kw};
+              off = e.kw ? tid * 16u : OOB;
+            } else {
+              off = OOB;
+              edge |= 1u << k;
+            }
+          } else {
+            off = OOB;
+          }
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(v ^ m, rs, off, k * G::NT * 16u, AUX_NT);
         // hipcc (ROCm 7.2, gfx950) may overwrite a dwordx4 store's data VGPRs
         // in the very next instruction; later lanes then store the new value
         // (seen as wrong bytes in dword 0, lanes 12-15 of each 16). Two wait
         // states after the store; inline asm is a scheduling boundary.
         asm volatile("s_nop 1" ::: "memory");
-        if (in && nz && !full) edge |= 1u << k;
       }
 #pragma nounroll
-      while (edge) {  // the batch's first/last chunk: only the bytes in [wl, whi)
+      while (edge) {  // chunks with a frame boundary, and the batch's first/last chunk
         const uint32_t k = __builtin_ctz(edge);
         edge &= edge - 1;
         const uint32_t a = (k * G::NT + tid) * 16u;
-        const uint64_t A = ss + a;
         uint32_t x = 0, y = nfl;
         while (y - x > 1) {
           const uint32_t mid = (x + y) >> 1;
           if (L.fl[mid].start <= a) x = mid; else y = mid;
         }
         const u32x4 m = chunk_xor(L, nfl, x, a);
+        if ((m.x | m.y | m.z | m.w) == 0u) continue;
+        if (a >= wl_r && a + 16 <= wh_r) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
+          __builtin_amdgcn_raw_buffer_store_b128(v ^ m, rs, tid * 16u, k * G::NT * 16u, AUX_NT);
+          asm volatile("s_nop 1" ::: "memory");
+          continue;
+        }
+        const uint64_t A = ss + a;
 #pragma nounroll
-        for (uint32_t t = 0; t < 16; t++) {
+        for (uint32_t t = 0; t < 16; t++) {  // only the bytes in [wl, whi)
           const uint64_t q = A + t;
           const uint32_t mw = t < 4 ? m.x : t < 8 ? m.y : t < 12 ? m.z : m.w;
           const uint8_t kb = (uint8_t)(mw >> (8u * (t & 3u)));
@@ -614,10 +698,10 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
         uint32_t c = nfl;
         while (c > 0 && L.fl[c - 1].end > hi_c) c--;
         for (uint32_t i = c; i < nfl; i++) L.fl[i - c] = L.fl[i];
-        L.aux2 = nfl - c;
+        L.keepn = nfl - c;
       }
       __syncthreads();
-      keep = (uint32_t)L.aux2;
+      keep = L.keepn;
       lo_c = hi_c;
     }
     // continue while bytes below the write limit remain
@@ -666,130 +750,202 @@ XYWS_DEV uint32_t chain_plausible(const run_params& P, const lds_t<G>& L, uint64
 // Candidate bits of the 16 positions of chunk a (bit t: position a + t).
 template <class G>
 XYWS_DEV uint32_t chunk_candidates(const run_params& P, const lds_t<G>& L, uint32_t a, bool unm) {
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(L.seg + a);
-  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
-  uint32_t bits = cand_nibble(w0, w1, unm) | (cand_nibble(w1, w2, unm) << 4) |
-                  (cand_nibble(w2, w3, unm) << 8) | (cand_nibble(w3, w4, unm) << 12);
+  const u32x4 v = *reinterpret_cast<const u32x4*>(L.seg + a);
+  const uint32_t w4 = *reinterpret_cast<const uint32_t*>(L.seg + a + 16);
+  uint32_t bits = cand_nibble(v.x, v.y, unm) | (cand_nibble(v.y, v.z, unm) << 4) |
+                  (cand_nibble(v.z, v.w, unm) << 8) | (cand_nibble(v.w, w4, unm) << 12);
   // headers straddling the segment end are left to the next segment's scan
   if (a + 16 + 1 > G::SEG) bits &= (1u << (G::SEG - XYWS_MAX_FRAME_HEADER_SIZE - a + 1)) - 1u;
   return bits;
 }
 
-// Prologue scan of the segment in LDS (see find_entry). mem = false: chains
-// leaving the segment are appended to L.ul (L.ucnt counts past UCAP on
-// overflow); mem = true: they are followed through memory.
+// Candidate bits of the 4 positions of dword w (wn: the next dword) at bits
+// 7, 15, 23, 31: the cand_nibble test with fewer operations.
+XYWS_DEV uint32_t cand_bytes(uint32_t w, uint32_t wn, bool unmasked) {
+  const uint32_t b1s = __builtin_amdgcn_alignbyte(wn, w, 1);               // byte t = byte t+1
+  const uint32_t rsv = ((w & 0x74747474u) + 0x7F7F7F7Fu);                    // RSV or opcode bit 2
+  const uint32_t b3 = (w << 7) & (w << 6);                                   // opcode & 3 == 3
+  const uint32_t ctl = (w << 4) & ~w;                                        // control without FIN
+  const uint32_t m = unmasked ? ~b1s : b1s;
+  return m & ~(rsv | b3 | ctl) & 0x80808080u;
+}
+
+// First byte pair of a client header (cand_nibble for one position).
+XYWS_DEV bool cand_pair(uint32_t b0, uint32_t b1, bool unm) {
+  return (b0 & 0x74u) == 0 && (b0 & 3u) != 3u && !((b0 & 0x08u) && !(b0 & 0x80u)) &&
+         ((b1 >> 7) != 0) != unm;
+}
+
+// Second-level filter for the candidate at segment offset p (cheap, from LDS):
+// false only when the header after it (7-bit or 126 form) lies in the segment
+// and the batch and fails cand_pair, i.e. when its chain is certainly
+// implausible (cand_pair is implied by plausible()).
 template <class G>
-XYWS_DEV void scan_windows(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid, bool unm, bool mem) {
+XYWS_DEV bool second_hop_ok(const run_params& P, const lds_t<G>& L, uint64_t ss, uint32_t p, bool unm) {
+  const uint32_t b1 = L.seg[p + 1], l7 = b1 & 0x7Fu;
+  uint32_t nxt;
+  if (l7 < 126) nxt = p + 2 + (unm ? 0u : 4u) + l7;
+  else if (l7 == 126) nxt = p + 4 + (unm ? 0u : 4u) + (((uint32_t)L.seg[p + 2] << 8) | L.seg[p + 3]);
+  else return true;
+  if (nxt + 2 > G::SEG || ss + nxt + 2 > P.hi) return true;
+  return cand_pair(L.seg[nxt], L.seg[nxt + 1], unm);
+}
+
+// Prologue scan of the segment at ss, in LDS (see find_entry): L.best = the
+// earliest offset whose chain of KHDR headers is plausible (0xFFFFFFFF: none).
+//  1. every lane filters its own CH chunks: candidate bits (SWAR) and the
+//     cheap second-hop test; survivors go to an LDS list;
+//  2. survivors' chains, one per lane, followed in LDS; chains leaving the
+//     segment are listed as undecided;
+//  3. undecided survivors below the best so far: chains followed through
+//     memory (one memory latency per segment).
+// A list overflow (e.g. a stream of 2-byte frames) falls back to each lane
+// checking its own candidates in order through memory.
+template <class G>
+XYWS_DEV void scan_segment(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid, bool unm) {
   const bool st_on = stats_on(P) && tid == 0;
-  uint64_t tq = st_on ? __builtin_amdgcn_s_memtime() : 0, a_comp = 0, a_check = 0, nwin = 0, ncand = 0;
-#pragma unroll 1
+  uint64_t tq = st_on ? __builtin_amdgcn_s_memtime() : 0;
+  if (tid == 0) { L.ccnt = 0; L.ucnt = 0; }
+  __syncthreads();
+  // Candidate bits of the lane's CH chunks (chunk k at segment offset
+  // (k*NT + tid)*16: conflict-free LDS reads), packed two chunks per word:
+  // bit 8*b + 4*h + i of m[k/2] = byte b of dword i of chunk 2*(k/2) + h.
+  constexpr uint32_t NM = (G::CH + 1) / 2;
+  // candidate offsets below qlim: the header fits the segment, the byte is in the batch
+  const uint64_t rel_hi = P.hi - ss;
+  const uint32_t qlim = rel_hi < G::SEG - XYWS_MAX_FRAME_HEADER_SIZE + 1 ? (uint32_t)rel_hi
+                                                                          : G::SEG - XYWS_MAX_FRAME_HEADER_SIZE + 1;
+  uint32_t m[NM];
+#pragma unroll
+  for (uint32_t g = 0; g < NM; g++) m[g] = 0;
+#pragma unroll
   for (uint32_t k = 0; k < G::CH; k++) {
-    const uint32_t wb = k * G::NT * 16u;
-    if (ss + wb >= P.hi) break;
-    const uint32_t a = wb + tid * 16u;
-    const uint32_t bits = ss + a < P.hi ? chunk_candidates<G>(P, L, a, unm) : 0u;
-    if (tid == 0) L.ccnt = 0;
-    __syncthreads();
-    uint32_t tot = 0;
-#pragma unroll
-    for (uint32_t t = 0; t < 16; t++) tot += __popcll(__ballot((bits >> t) & 1u));
-    uint32_t base = 0;
-    if ((tid & 63u) == 0 && tot) base = atomicAdd(&L.ccnt, tot);
-    base = __shfl(base, 0);
-#pragma unroll
-    for (uint32_t t = 0; t < 16; t++) {
-      const uint64_t m = __ballot((bits >> t) & 1u);
-      const uint32_t i = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      if (((bits >> t) & 1u) && i < CCAP) L.cl[i] = (uint16_t)(tid * 16u + t);
-      base += __popcll(m);
+    const uint32_t a = (k * G::NT + tid) * 16u;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(L.seg + a);
+    const uint32_t w4 = *reinterpret_cast<const uint32_t*>(L.seg + a + 16);
+    const uint32_t h = (k & 1u) * 4u;
+    uint32_t c = (cand_bytes(v.x, v.y, unm) >> (7 - h)) | (cand_bytes(v.y, v.z, unm) >> (6 - h)) |
+                 (cand_bytes(v.z, v.w, unm) >> (5 - h)) | (cand_bytes(v.w, w4, unm) >> (4 - h));
+    // headers straddling the segment end are left to the next segment's scan;
+    // none past the batch end
+    if (a + 16 > qlim) {
+      uint32_t keep = 0;
+#pragma unroll 1
+      for (uint32_t t = 0; a + t < qlim && t < 16; t++) keep |= 1u << (8u * (t & 3u) + h + (t >> 2));
+      c &= keep;
     }
-    __syncthreads();
-    const uint32_t n = L.ccnt;
-    if (st_on) {
-      const uint64_t t = __builtin_amdgcn_s_memtime();
-      if (k == 0) stat_add(P, ST_P_TRES, t - tq);
-      a_comp += t - tq; tq = t; nwin++; ncand += n;
+    m[k / 2] |= c;
+  }
+  // every candidate: the second-hop test; survivors go to the LDS list (one
+  // loop over all words: a wave iterates as often as its busiest lane)
+  uint32_t any = 0;
+#pragma unroll
+  for (uint32_t g = 0; g < NM; g++) any |= m[g];
+  while (any) {
+    uint32_t b = m[0], g = 0;
+#pragma unroll
+    for (uint32_t j = NM - 1; j >= 1; j--) {
+      if (m[j]) { b = m[j]; g = j; }  // the lowest non-empty word wins
     }
-    auto check = [&](uint32_t pos) {
-      const uint32_t v = chain_plausible(P, L, ss, ss + pos, unm, mem);
-      if (v == 1u) {
-        atomicMin(&L.best, pos);
-      } else if (v == 2u) {
-        const uint32_t u = atomicAdd(&L.ucnt, 1u);
-        if (u < UCAP) L.ul[u] = pos;
-      }
-      return v == 1u;
-    };
-    if (n <= CCAP) {
-      for (uint32_t i = tid; i < n; i += G::NT) {
-        const uint32_t pos = wb + L.cl[i];
-        if (pos < __hip_atomic_load(&L.best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) check(pos);
-      }
-    } else {  // more candidates than the list holds: each lane checks its own
-      uint32_t b = bits;
+    if (m[0]) { b = m[0]; g = 0; }
+    const uint32_t t = __builtin_ctz(b);
+    const uint32_t bit = b & (0u - b);
+#pragma unroll
+    for (uint32_t j = 0; j < NM; j++)
+      if (g == j) m[j] &= ~bit;
+    any = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < NM; j++) any |= m[j];
+    const uint32_t k = 2 * g + ((t >> 2) & 1u), i = t & 3u, byte = t >> 3;
+    const uint32_t pos = (k * G::NT + tid) * 16u + 4u * i + byte;
+    if (second_hop_ok<G>(P, L, ss, pos, unm)) {
+      const uint32_t slot = atomicAdd(&L.ccnt, 1u);
+      if (slot < SCAP) L.sl[slot] = pos;
+    }
+  }
+  __syncthreads();
+  const uint32_t n = L.ccnt;
+  if (st_on) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    stat_add(P, ST_P_TCOMP, t - tq); stat_add(P, ST_P_CAND, n); stat_add(P, ST_P_WIN, 1);
+    tq = t;
+  }
+  if (n > SCAP) {  // overflow: per lane, in order, through memory
+#pragma unroll 1
+    for (uint32_t k = 0; k < G::CH; k++) {
+      const uint32_t a = (k * G::NT + tid) * 16u;
+      uint32_t b = ss + a < P.hi ? chunk_candidates<G>(P, L, a, unm) : 0u;
+      bool hit = false;
       while (b) {
         const uint32_t t = __builtin_ctz(b);
         b &= b - 1;
-        if (check(a + t)) break;
+        const uint32_t pos = a + t;
+        if (pos > __hip_atomic_load(&L.best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { hit = true; break; }
+        if (chain_plausible(P, L, ss, ss + pos, unm, true) == 1u) {
+          atomicMin(&L.best, pos);
+          hit = true;
+          break;
+        }
       }
+      if (hit) break;
     }
     __syncthreads();
-    if (st_on) {
-      const uint64_t t = __builtin_amdgcn_s_memtime();
-      a_check += t - tq; tq = t;
-    }
-    if (L.best != 0xFFFFFFFFu) break;
+    return;
   }
+  for (uint32_t i = tid; i < n; i += G::NT) {
+    const uint32_t pos = L.sl[i];
+    if (pos > __hip_atomic_load(&L.best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) continue;
+    const uint32_t v = chain_plausible(P, L, ss, ss + pos, unm, false);
+    if (v == 1u) {
+      atomicMin(&L.best, pos);
+    } else if (v == 2u) {
+      const uint32_t u = atomicAdd(&L.ucnt, 1u);
+      if (u < UCAP) L.ul[u] = pos;
+    }
+  }
+  __syncthreads();
+  const uint32_t nu = L.ucnt, best = L.best;
   if (st_on) {
-    stat_add(P, ST_P_WIN, nwin); stat_add(P, ST_P_CAND, ncand);
-    stat_add(P, ST_P_TCOMP, a_comp); stat_add(P, ST_P_TCHECK, a_check);
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    stat_add(P, ST_P_TCHECK, t - tq); stat_add(P, ST_P_UND, nu);
+    tq = t;
+  }
+  if (nu) {
+    // (an overflowed undecided list: every survivor below best again, through memory)
+    const uint32_t m = nu > UCAP ? n : nu;
+    for (uint32_t i = tid; i < m; i += G::NT) {
+      const uint32_t pos = nu > UCAP ? L.sl[i] : L.ul[i];
+      if (pos < best && chain_plausible(P, L, ss, ss + pos, unm, true) == 1u) atomicMin(&L.best, pos);
+    }
+    __syncthreads();
+    if (st_on) stat_add(P, ST_P_TRES, __builtin_amdgcn_s_memtime() - tq);
   }
 }
 
 template <class G>
 XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint32_t run) {
   const bool unm = (P.opts & XYWS_OPT_UNMASKED_HINT) != 0;
-  const uint64_t s_begin = (uint64_t)run * P.spr;
-  uint64_t s_end = s_begin + P.spr;
-  if (s_end > P.nseg) s_end = P.nseg;
+  const uint64_t rb = (uint64_t)run * P.rbytes;
+  uint64_t re = rb + P.rbytes;
+  if (re > P.hi) re = P.hi;
   if (tid == 0) L.aux0 = NONE;
   uint64_t tp = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
-  for (uint64_t s = s_begin; s < s_end; s++) {
-    const uint64_t ss = s * G::SEG;
+  for (uint64_t ss = rb; ss < re; ss += G::SEG) {
     __syncthreads();
-    io.fill(P, L, s, tid);
-    if (tid == 0) { L.best = 0xFFFFFFFFu; L.aux1 = s; }
+    io.fill(P, L, ss, tid);
+    if (tid == 0) { L.best = 0xFFFFFFFFu; L.aux1 = ss; }
     __syncthreads();
     if (stats_on(P) && tid == 0) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       stat_add(P, ST_P_FILL, t - tp);
       tp = t;
     }
-    // (no prefetch during the scan: a header read from memory, and the
-    // publish's vmcnt(0), would wait for it)
-    // One window of NT chunks (16 B per thread, contiguous) at a time: the
-    // window's candidates are compacted into an LDS list and their chains are
-    // checked one candidate per lane (a per-thread loop would make every wave
-    // wait for its lane with the most candidates); the earliest plausible one
-    // wins, and windows are in position order, so the first window with a
-    // winner ends the scan. Chains are followed in LDS only; candidates whose
-    // chain leaves the segment are listed and resolved from memory afterwards,
-    // all at once (one memory latency for the scan, not one per window).
-    if (tid == 0) L.ucnt = 0;
-    scan_windows<G>(P, L, ss, tid, unm, false);
-    const uint32_t nu = L.ucnt;
-    if (stats_on(P) && tid == 0) stat_add(P, ST_P_UND, nu);
-    if (nu > UCAP) {  // the list overflowed: scan again following chains through memory
-      scan_windows<G>(P, L, ss, tid, unm, true);
-    } else if (nu) {
-      const uint32_t best = L.best;
-      for (uint32_t i = tid; i < nu; i += G::NT) {
-        const uint32_t pos = L.ul[i];
-        if (pos < best && chain_plausible(P, L, ss, ss + pos, unm, true) == 1u) atomicMin(&L.best, pos);
-      }
-    }
-    __syncthreads();
+    // the next segment's loads fly during the scan: the chain starts there when
+    // the entry is in this segment, the scan continues there when it is not
+    // (HBM would idle during the scan otherwise; the few header reads from
+    // memory below and the publish's vmcnt(0) wait for them)
+    if (ss + G::SEG < P.hi && !(P.opts & XYWS_OPT_DIAG)) io.issue(P, ss + G::SEG, tid);
+    scan_segment<G>(P, L, ss, tid, unm);
     if (stats_on(P) && tid == 0) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       stat_add(P, ST_P_SCAN, t - tp);
@@ -815,10 +971,10 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
   if (run >= P.nruns) return;
   uint64_t* rec = P.rec + (uint64_t)run * R_WORDS;
   if (tid == 0) st_store(rec + R_ECNT, 0);  // no descriptors unless k_stream_finish plans them
-  const uint64_t rng_end = run + 1 < P.nruns ? (uint64_t)(run + 1) * P.spr * G::SEG : NONE;
+  const uint64_t rng_end = run + 1 < P.nruns ? (uint64_t)(run + 1) * P.rbytes : NONE;
   seg_io<G> io;
   uint64_t t0 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
-  uint64_t wlo, s0;
+  uint64_t wlo, ss0;
   bool in_lds = false;
   if (run == 0) {
     if (tid == 0) {
@@ -840,13 +996,12 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
       st_store(rec + R_HEAD, c0);
     }
     wlo = P.lo;
-    s0 = 0;
+    ss0 = 0;
   } else {
     find_entry(P, L, io, tid, run);
     const uint64_t tpub = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
     if (tid == 0) {
-      const uint64_t q = L.aux0, seg_q = L.aux1;
-      const uint64_t ss = seg_q * G::SEG;
+      const uint64_t q = L.aux0, ss = L.aux1;
       uint64_t h = NONE, W = NONE, hc = 0;
       cstate S;
       S.X = 0; S.cov_ps = 0; S.cov_start = 0; S.cov_kw = 0; S.cov_key = 0; S.st = S_NOCOV; S.pad = 0;
@@ -886,10 +1041,11 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
     __syncthreads();
     if (L.aux2 == NONE) return;  // no entry: the chain of an earlier run covers this range
     wlo = L.aux2;
-    s0 = wlo / G::SEG;
-    in_lds = s0 == L.aux1;
-    // published: now the next segment's loads
-    if (in_lds && (s0 + 1) * G::SEG < P.hi) io.issue(P, s0 + 1, tid);
+    // the chain starts in the scanned segment (usual) or on the grid after it
+    ss0 = L.aux1 + (wlo - L.aux1) / G::SEG * G::SEG;
+    in_lds = ss0 == L.aux1;
+    // (the next segment's loads were issued before the scan)
+    if (in_lds && ss0 + G::SEG < P.hi && io.pf != ss0 + G::SEG) io.issue(P, ss0 + G::SEG, tid);
   }
   if (tid == 0) {
     L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.first_after = NONE;
@@ -898,7 +1054,7 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
   }
   __syncthreads();
   uint64_t t1 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
-  run_chain(P, L, io, tid, s0, in_lds, wlo, rng_end, run);
+  run_chain(P, L, io, tid, ss0, in_lds, wlo, rng_end, run);
   if (tid == 0) {
     const bool ok = L.succ >= P.nruns || (L.past && L.ok);
     st_store(rec + R_OK, (uint64_t)(ok ? 1u : 0u) | ((uint64_t)L.succ << 32));
@@ -1049,7 +1205,7 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
     const uint64_t W = st_load(rs + R_W);
     const uint64_t hn = L.hn, Wn = L.Wn, succ = L.succ;
     io.pf = NONE;
-    run_chain(P, L, io, tid, W / G::SEG, false, W, NONE, 0);
+    run_chain(P, L, io, tid, W & ~15ull, false, W, NONE, 0);
     __threadfence();  // the undo's stores are visible to the redo's loads
     __syncthreads();
     // redo from the exact state, same successor
@@ -1063,7 +1219,7 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
     }
     __syncthreads();
     io.pf = NONE;
-    run_chain(P, L, io, tid, W / G::SEG, false, W, NONE, 0);
+    run_chain(P, L, io, tid, W & ~15ull, false, W, NONE, 0);
     __threadfence();
     __syncthreads();
   }
@@ -1242,6 +1398,14 @@ int stream_scratch_stats(stream_scratch* s, uint64_t out[32]) {
              ? XYWS_OK : XYWS_ERR_HIP;
 }
 
+int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_runs) {
+  if (!s->mem) return XYWS_ERR_INVALID;
+  if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
+  const uint64_t n = max_runs < s->max_runs ? max_runs : s->max_runs;
+  const uint8_t* rec = static_cast<const uint8_t*>(s->mem) + HEAD_BYTES + flags_bytes(s->max_runs);
+  return hipMemcpy(out, rec, n * R_WORDS * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int64_t)n : XYWS_ERR_HIP;
+}
+
 uint32_t stream_scratch_error(stream_scratch* s) {
   if (!s->mem) return 0;
   uint32_t v[2] = {0, 0};
@@ -1259,16 +1423,19 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   const bool small = (opts & XYWS_OPT_SMALL_SEG) != 0;
   const bool wg512 = !small && (opts & XYWS_OPT_WG512) != 0;
   const uint64_t seg = small ? G_SMALL::SEG : wg512 ? G_PROD2::SEG : G_PROD::SEG;
+  // Runs get equal byte ranges (multiples of 16, one segment at least): every
+  // workgroup streams the same number of bytes, and a run whose chain crosses
+  // into the next range loads only the bytes below the successor's W there.
   const uint64_t nseg = (hi + seg - 1) / seg;
-  uint64_t nruns, spr;
-  if (small) {
-    nruns = nseg;
-    spr = 1;
+  uint64_t nruns, rbytes;
+  const uint64_t r = small ? nseg : (uint64_t)s->ncu * (wg512 ? 2u : 1u);
+  const uint64_t maxr = r < MAX_RUNS ? r : MAX_RUNS;
+  if (nseg <= maxr) {
+    rbytes = seg;
   } else {
-    const uint64_t r = (uint64_t)s->ncu * (wg512 ? 2u : 1u), maxr = r < MAX_RUNS ? r : MAX_RUNS;
-    spr = (nseg + maxr - 1) / maxr;
-    nruns = (nseg + spr - 1) / spr;
+    rbytes = ((hi + maxr - 1) / maxr + 15) & ~15ull;
   }
+  nruns = (hi + rbytes - 1) / rbytes;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(stream, &cs);
   if (nruns > s->max_runs || !s->mem) {
@@ -1278,8 +1445,8 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   }
   uint8_t* m = static_cast<uint8_t*>(s->mem);
   run_params P;
-  P.base = base; P.lo = lo; P.hi = hi; P.nseg = nseg;
-  P.nruns = (uint32_t)nruns; P.spr = (uint32_t)spr;
+  P.base = base; P.lo = lo; P.hi = hi; P.rbytes = rbytes;
+  P.nruns = (uint32_t)nruns;
   P.cout = cout; P.frames = frames; P.cap = cap; P.nframes = nframes;
   P.head = reinterpret_cast<uint32_t*>(m);
   P.flags = reinterpret_cast<uint32_t*>(m + HEAD_BYTES);
