@@ -152,12 +152,11 @@ struct __attribute__((aligned(16))) lds_t {
   cstate S;
   cstate B;  // k_stream_finish: exact state handed to a repaired run
   uint64_t hn, Wn, succ, first_after, cnt, tail, aux0, aux1, aux2, bcnt, bfirst;
-  uint32_t nfl, pass_hi, known, past, ok, done, end, best, ticket, act, repaired, ccnt, ucnt, keepn;
+  uint32_t nfl, pass_hi, known, past, ok, done, end, best, ticket, act, repaired, ccnt, ucnt, keepn, ovf;
   // per 1 KiB row of the segment (one wave-instruction of chunks), set by
   // wave 0 after each chase pass: ROW_FAST (one key word for the whole row,
   // rk), ROW_SKIP (nothing to store) or the entry to start the walk from
-  uint32_t rt[G::SEG / 1024];
-  uint32_t rk[G::SEG / 1024];
+  uint2 rt[G::SEG / 1024];  // (class or entry, key word)
 };
 
 // ---------------------------------------------------------------- small helpers
@@ -485,8 +484,7 @@ XYWS_DEV void build_rows(lds_t<G>& L, uint32_t nfl, uint32_t lo_c, uint32_t hi_c
         kw = e.kw;
       }
     }
-    L.rt[r] = info;
-    L.rk[r] = kw;
+    L.rt[r] = uint2{info, kw};
   }
 }
 
@@ -616,16 +614,25 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
       // this unrolled loop: the next segment's loads are in flight).
       uint32_t edge = 0;
       const uint32_t wave = tid >> 6;
+      u32x4 dprev = {0u, 0u, 0u, 0u};
+      // software pipeline: chunk k+1's row word and bytes are read from LDS
+      // before chunk k's store
+      uint2 rw_n = L.rt[wave];
+      u32x4 v_n = *reinterpret_cast<const u32x4*>(&L.seg[tid * 16u]);
 #pragma unroll
       for (uint32_t k = 0; k < G::CH; k++) {
         const uint32_t a = (k * G::NT + tid) * 16u;
-        const uint32_t row = k * (G::NT / 64) + wave;
-        const uint32_t info = __builtin_amdgcn_readfirstlane(L.rt[row]);
-        const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
+        const uint2 rw = rw_n;
+        const u32x4 v = v_n;
+        if (k + 1 < G::CH) {
+          rw_n = L.rt[(k + 1) * (G::NT / 64) + wave];
+          v_n = *reinterpret_cast<const u32x4*>(&L.seg[((k + 1) * G::NT + tid) * 16u]);
+        }
+        const uint32_t info = __builtin_amdgcn_readfirstlane(rw.x);
+        const uint32_t kw = __builtin_amdgcn_readfirstlane(rw.y);
         u32x4 m;
         uint32_t off;
         if (info & ROW_FAST) {
-          const uint32_t kw = __builtin_amdgcn_readfirstlane(L.rk[row]);
           m = u32x4{kw, kw, kw, kw};
           off = tid * 16u;
         } else if (info & ROW_SKIP) {
@@ -657,13 +664,17 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
             off = OOB;
           }
         }
-        __builtin_amdgcn_raw_buffer_store_b128(v ^ m, rs, off, k * G::NT * 16u, AUX_NT);
+        const u32x4 d = v ^ m;
+        __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, k * G::NT * 16u, AUX_NT);
         // hipcc (ROCm 7.2, gfx950) may overwrite a dwordx4 store's data VGPRs
         // in the very next instruction; later lanes then store the new value
-        // (seen as wrong bytes in dword 0, lanes 12-15 of each 16). Two wait
-        // states after the store; inline asm is a scheduling boundary.
-        asm volatile("s_nop 1" ::: "memory");
+        // (seen as wrong bytes in dword 0, lanes 12-15 of each 16). The data
+        // stays live until after the next chunk's store (an empty asm use, no
+        // memory clobber: the next chunk's LDS reads may still be hoisted).
+        asm volatile("" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
+        dprev = d;
       }
+      asm volatile("s_nop 1" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
 #pragma nounroll
       while (edge) {  // chunks with a frame boundary, and the batch's first/last chunk
         const uint32_t k = __builtin_ctz(edge);
@@ -793,84 +804,141 @@ XYWS_DEV bool second_hop_ok(const run_params& P, const lds_t<G>& L, uint64_t ss,
 
 // Prologue scan of the segment at ss, in LDS (see find_entry): L.best = the
 // earliest offset whose chain of KHDR headers is plausible (0xFFFFFFFF: none).
-//  1. every lane filters its own CH chunks: candidate bits (SWAR) and the
-//     cheap second-hop test; survivors go to an LDS list;
+//  first for the segment's first NT chunks, then (no winner) for the rest:
+//  1. every lane filters its chunks: candidate bits (SWAR) and the cheap
+//     second-hop test; survivors go to an LDS list;
 //  2. survivors' chains, one per lane, followed in LDS; chains leaving the
 //     segment are listed as undecided;
-//  3. undecided survivors below the best so far: chains followed through
+//  then 3. undecided survivors below the best so far: chains followed through
 //     memory (one memory latency per segment).
 // A list overflow (e.g. a stream of 2-byte frames) falls back to each lane
 // checking its own candidates in order through memory.
 template <class G>
 XYWS_DEV void scan_segment(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid, bool unm) {
   const bool st_on = stats_on(P) && tid == 0;
-  uint64_t tq = st_on ? __builtin_amdgcn_s_memtime() : 0;
-  if (tid == 0) { L.ccnt = 0; L.ucnt = 0; }
-  __syncthreads();
-  // Candidate bits of the lane's CH chunks (chunk k at segment offset
-  // (k*NT + tid)*16: conflict-free LDS reads), packed two chunks per word:
-  // bit 8*b + 4*h + i of m[k/2] = byte b of dword i of chunk 2*(k/2) + h.
-  constexpr uint32_t NM = (G::CH + 1) / 2;
+  uint64_t tq = st_on ? __builtin_amdgcn_s_memtime() : 0, a_filt = 0, a_chk = 0, nwin = 0, nsurv = 0;
+  if (tid == 0) { L.ucnt = 0; L.ovf = 0; }
   // candidate offsets below qlim: the header fits the segment, the byte is in the batch
   const uint64_t rel_hi = P.hi - ss;
   const uint32_t qlim = rel_hi < G::SEG - XYWS_MAX_FRAME_HEADER_SIZE + 1 ? (uint32_t)rel_hi
                                                                           : G::SEG - XYWS_MAX_FRAME_HEADER_SIZE + 1;
-  uint32_t m[NM];
-#pragma unroll
-  for (uint32_t g = 0; g < NM; g++) m[g] = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < G::CH; k++) {
+  // Candidate bits of chunk k (segment offset (k*NT + tid)*16: conflict-free
+  // LDS reads), bit 8*b + h + i = byte b of dword i (h: a 4-bit lane of the
+  // packed word).
+  auto chunk_bits = [&](uint32_t k, uint32_t h) -> uint32_t {
     const uint32_t a = (k * G::NT + tid) * 16u;
+    if (ss + a >= P.hi) return 0u;
     const u32x4 v = *reinterpret_cast<const u32x4*>(L.seg + a);
     const uint32_t w4 = *reinterpret_cast<const uint32_t*>(L.seg + a + 16);
-    const uint32_t h = (k & 1u) * 4u;
     uint32_t c = (cand_bytes(v.x, v.y, unm) >> (7 - h)) | (cand_bytes(v.y, v.z, unm) >> (6 - h)) |
                  (cand_bytes(v.z, v.w, unm) >> (5 - h)) | (cand_bytes(v.w, w4, unm) >> (4 - h));
-    // headers straddling the segment end are left to the next segment's scan;
-    // none past the batch end
     if (a + 16 > qlim) {
       uint32_t keep = 0;
 #pragma unroll 1
       for (uint32_t t = 0; a + t < qlim && t < 16; t++) keep |= 1u << (8u * (t & 3u) + h + (t >> 2));
       c &= keep;
     }
-    m[k / 2] |= c;
-  }
-  // every candidate: the second-hop test; survivors go to the LDS list (one
-  // loop over all words: a wave iterates as often as its busiest lane)
-  uint32_t any = 0;
-#pragma unroll
-  for (uint32_t g = 0; g < NM; g++) any |= m[g];
-  while (any) {
-    uint32_t b = m[0], g = 0;
-#pragma unroll
-    for (uint32_t j = NM - 1; j >= 1; j--) {
-      if (m[j]) { b = m[j]; g = j; }  // the lowest non-empty word wins
-    }
-    if (m[0]) { b = m[0]; g = 0; }
-    const uint32_t t = __builtin_ctz(b);
-    const uint32_t bit = b & (0u - b);
-#pragma unroll
-    for (uint32_t j = 0; j < NM; j++)
-      if (g == j) m[j] &= ~bit;
-    any = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < NM; j++) any |= m[j];
-    const uint32_t k = 2 * g + ((t >> 2) & 1u), i = t & 3u, byte = t >> 3;
-    const uint32_t pos = (k * G::NT + tid) * 16u + 4u * i + byte;
+    return c;
+  };
+  auto survivor = [&](uint32_t pos) {
     if (second_hop_ok<G>(P, L, ss, pos, unm)) {
       const uint32_t slot = atomicAdd(&L.ccnt, 1u);
       if (slot < SCAP) L.sl[slot] = pos;
     }
-  }
+  };
+  // survivors' chains in LDS, one per lane; chains leaving the segment are
+  // listed as undecided; true when the scan is over (a winner, or overflow)
+  auto check = [&]() -> bool {
+    __syncthreads();
+    const uint32_t n = L.ccnt;
+    if (st_on) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      a_filt += t - tq; tq = t; nwin++; nsurv += n;
+    }
+    if (n > SCAP) {
+      if (tid == 0) L.ovf = 1;
+    } else {
+      // (i is opaque to the compiler: a hoisted, spilled &L.sl[tid] would be
+      // reloaded behind a vmcnt(0) that waits for the prefetch in flight)
+      uint32_t i0 = tid;
+      asm volatile("" : "+v"(i0));
+      for (uint32_t i = i0; i < n; i += G::NT) {
+        const uint32_t pos = L.sl[i];
+        if (pos > __hip_atomic_load(&L.best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) continue;
+        const uint32_t r = chain_plausible(P, L, ss, ss + pos, unm, false);
+        if (r == 1u) {
+          atomicMin(&L.best, pos);
+        } else if (r == 2u) {
+          const uint32_t u = atomicAdd(&L.ucnt, 1u);
+          if (u < UCAP) L.ul[u] = pos;
+          else L.ovf = 1;
+        }
+      }
+    }
+    __syncthreads();
+    if (st_on) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      a_chk += t - tq; tq = t;
+    }
+    return L.ovf || L.best != 0xFFFFFFFFu;
+  };
+  // Window 0 (the first NT chunks, 16 KiB for 1024 lanes) alone first: a
+  // chain usually starts within one frame of the range start. Then the rest
+  // of the segment in one pass, each lane's candidates in one loop (a wave
+  // iterates as often as its busiest lane).
+  if (tid == 0) L.ccnt = 0;
   __syncthreads();
-  const uint32_t n = L.ccnt;
-  if (st_on) {
-    const uint64_t t = __builtin_amdgcn_s_memtime();
-    stat_add(P, ST_P_TCOMP, t - tq); stat_add(P, ST_P_CAND, n); stat_add(P, ST_P_WIN, 1);
-    tq = t;
+  {
+    uint32_t c = chunk_bits(0, 0);
+    while (c) {
+      const uint32_t t = __builtin_ctz(c);
+      c &= c - 1;
+      survivor(tid * 16u + 4u * (t & 3u) + (t >> 3));
+    }
   }
-  if (n > SCAP) {  // overflow: per lane, in order, through memory
+  bool over = check();
+  if constexpr (G::CH > 1) if (!over && ss + G::NT * 16u < P.hi) {
+    if (tid == 0) L.ccnt = 0;
+    __syncthreads();
+    // chunks 1..CH-1 packed two per word: m[j] holds chunks 2j+1 (h = 0) and 2j+2 (h = 4)
+    constexpr uint32_t NM = G::CH / 2;
+    uint32_t m[NM > 0 ? NM : 1];
+#pragma unroll
+    for (uint32_t j = 0; j < NM; j++)
+      m[j] = chunk_bits(2 * j + 1, 0) | (2 * j + 2 < G::CH ? chunk_bits(2 * j + 2, 4) : 0u);
+    uint32_t any = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < NM; j++) any |= m[j];
+    while (any) {
+      uint32_t b = m[0], g = 0;
+#pragma unroll
+      for (uint32_t j = NM - 1; j >= 1; j--) {
+        if (m[j]) { b = m[j]; g = j; }  // the lowest non-empty word wins
+      }
+      if (m[0]) { b = m[0]; g = 0; }
+      const uint32_t t = __builtin_ctz(b);
+      const uint32_t bit = b & (0u - b);
+#pragma unroll
+      for (uint32_t j = 0; j < NM; j++)
+        if (g == j) m[j] &= ~bit;
+      any = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < NM; j++) any |= m[j];
+      const uint32_t k = 2 * g + 1 + ((t >> 2) & 1u);
+      survivor((k * G::NT + tid) * 16u + 4u * (t & 3u) + (t >> 3));
+    }
+    (void)check();
+  }
+  if (st_on) {
+    stat_add(P, ST_P_TCOMP, a_filt); stat_add(P, ST_P_TCHECK, a_chk);
+    stat_add(P, ST_P_WIN, nwin); stat_add(P, ST_P_CAND, nsurv); stat_add(P, ST_P_UND, L.ucnt);
+  }
+  if (L.ovf) {
+    // a list overflowed (e.g. a stream of 2-byte frames): each lane checks its
+    // own candidates in order, through memory, from scratch
+    __syncthreads();
+    if (tid == 0) L.best = 0xFFFFFFFFu;
+    __syncthreads();
 #pragma unroll 1
     for (uint32_t k = 0; k < G::CH; k++) {
       const uint32_t a = (k * G::NT + tid) * 16u;
@@ -892,29 +960,11 @@ XYWS_DEV void scan_segment(const run_params& P, lds_t<G>& L, uint64_t ss, uint32
     __syncthreads();
     return;
   }
-  for (uint32_t i = tid; i < n; i += G::NT) {
-    const uint32_t pos = L.sl[i];
-    if (pos > __hip_atomic_load(&L.best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) continue;
-    const uint32_t v = chain_plausible(P, L, ss, ss + pos, unm, false);
-    if (v == 1u) {
-      atomicMin(&L.best, pos);
-    } else if (v == 2u) {
-      const uint32_t u = atomicAdd(&L.ucnt, 1u);
-      if (u < UCAP) L.ul[u] = pos;
-    }
-  }
-  __syncthreads();
+  // 3. undecided candidates below the best: chains through memory, all at once
   const uint32_t nu = L.ucnt, best = L.best;
-  if (st_on) {
-    const uint64_t t = __builtin_amdgcn_s_memtime();
-    stat_add(P, ST_P_TCHECK, t - tq); stat_add(P, ST_P_UND, nu);
-    tq = t;
-  }
   if (nu) {
-    // (an overflowed undecided list: every survivor below best again, through memory)
-    const uint32_t m = nu > UCAP ? n : nu;
-    for (uint32_t i = tid; i < m; i += G::NT) {
-      const uint32_t pos = nu > UCAP ? L.sl[i] : L.ul[i];
+    for (uint32_t i = tid; i < nu; i += G::NT) {
+      const uint32_t pos = L.ul[i];
       if (pos < best && chain_plausible(P, L, ss, ss + pos, unm, true) == 1u) atomicMin(&L.best, pos);
     }
     __syncthreads();
