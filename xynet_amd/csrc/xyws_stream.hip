@@ -419,6 +419,60 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   bool past = L.past != 0, done = false, end = false;
   uint64_t cnt = 0, tail = 0;
   for (;;) {
+    {
+      // Fast path (many frames per segment): 32-bit segment-relative parse of
+      // headers whose 14 bytes lie in LDS, in the batch and below the write
+      // limit, before the successor's entry; anything else (a length of 2^31
+      // or more, a limit, the segment end) goes to the general step below.
+      uint64_t fstop = se - XYWS_MAX_FRAME_HEADER_SIZE + 1;
+      const uint64_t hlim = P.hi < lim ? P.hi : lim;
+      if (hlim < fstop + XYWS_MAX_FRAME_HEADER_SIZE - 1)
+        fstop = hlim >= XYWS_MAX_FRAME_HEADER_SIZE - 1 ? hlim - (XYWS_MAX_FRAME_HEADER_SIZE - 1) : 0;
+      if (known && !past && hn < fstop) fstop = hn;
+      const uint64_t X0 = S.X;
+      if (!(S.st & (S_PARTIAL | S_CUT)) && X0 >= ss && X0 < fstop) {
+        const uint32_t st = (uint32_t)(fstop - ss);
+        uint32_t x = (uint32_t)(X0 - ss), lx = 0, lps = 0, lkey = 0, lkw = 0, k = 0;
+        while (x < st && n < FCAP) {
+          const uint32_t* q = reinterpret_cast<const uint32_t*>(L.seg + (x & ~3u));
+          const uint32_t sh = x & 3u, r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+          const uint32_t w0 = __builtin_amdgcn_alignbyte(r1, r0, sh), w1 = __builtin_amdgcn_alignbyte(r2, r1, sh);
+          const uint32_t b1 = (w0 >> 8) & 0xFFu, l7 = b1 & 0x7Fu, msk = b1 >> 7;
+          uint32_t plen, ext;
+          if (l7 < 126) {
+            plen = l7; ext = 0;
+          } else if (l7 == 126) {
+            plen = ((w0 >> 8) & 0xFF00u) | (w0 >> 24); ext = 2;
+          } else {
+            const uint32_t w2 = __builtin_amdgcn_alignbyte(r3, r2, sh);
+            const uint32_t hi32 = __builtin_amdgcn_alignbyte(w1, w0, 2);   // bytes 2..5
+            const uint32_t lo32 = __builtin_amdgcn_alignbyte(w2, w1, 2);   // bytes 6..9
+            if (hi32 != 0u || (lo32 & 0x80u)) break;                        // >= 2^31: general step
+            plen = __builtin_bswap32(lo32); ext = 8;
+          }
+          const uint32_t hl = 2 + ext + 4 * msk, ps = x + hl;
+          uint32_t key = 0;
+          if (msk) {
+            if (ext == 0) key = __builtin_amdgcn_alignbyte(w1, w0, 2);
+            else if (ext == 2) key = w1;
+            else key = __builtin_amdgcn_alignbyte(__builtin_amdgcn_alignbyte(r4, r3, sh),
+                                                  __builtin_amdgcn_alignbyte(r3, r2, sh), 2);
+          }
+          const uint32_t kw = rotr8(key, 0u - ps);  // aligned_key: ss is 16-byte aligned
+          fent e;
+          e.start = x; e.ps = ps; e.end = ps + plen; e.kw = kw;
+          L.fl[n++] = e;
+          lx = x; lps = ps; lkey = key; lkw = kw;
+          x = ps + plen;
+          k++;
+        }
+        if (k) {
+          S.cov_start = ss + lx; S.cov_ps = ss + lps; S.X = ss + x;
+          S.cov_key = lkey; S.cov_kw = lkw; S.st = 0;
+          if (past) tail += k; else cnt += k;
+        }
+      }
+    }
     const uint64_t X = S.X;
     if (known && !past && X >= hn) {  // the chain reached the successor's entry
       past = true;
