@@ -263,11 +263,12 @@ def main():
     avg_ms = sum(kernel_ms) / len(kernel_ms)
 
     if args.stats and rank == 0:  # one extra counted decode pair (keeps the step parity)
-        names = ["runs", "runs_without_entry", "bad_boundaries", "repairs", "cuts", "spins", "segments",
+        names = ["runs", "runs_without_entry", "bad_boundaries", "repairs", "cuts", "spins", "dense_passes",
                  "frames", "scan_segments", "scan_survivors", "scan_undecided", "cyc_scan_filter",
-                 "cyc_scan_check", "cyc_scan_resolve", "-", "-", "cyc_prologue", "cyc_main", "cyc_wait",
+                 "cyc_scan_check", "cyc_scan_resolve", "cyc_dense_entry", "cyc_dense_chase", "cyc_prologue", "cyc_main", "cyc_wait",
                  "cyc_fill", "cyc_chase_sync", "cyc_xor", "cyc_tail", "cyc_prefetch_issue", "cyc_chase_pass",
-                 "cyc_pro_fill", "cyc_pro_scan", "cyc_pro_publish"]
+                 "cyc_pro_fill", "cyc_pro_scan", "cyc_pro_publish", "dense_no_entry", "dense_chase_fail",
+                 "dense_mismatch", "dense_overflow"]
         for _ in range(2):
             dec.opts |= 0x100
             dec.decode(buf, cap=0, count=False, carry=False)

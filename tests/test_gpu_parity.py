@@ -157,6 +157,40 @@ def test_fuzz_random_streams_vs_oracle(ws, oracle, mode):
             assert carry_list(dec.carry()) == carry_list(carry)
 
 
+@pytest.mark.parametrize("fake", [0, 1, 2])
+def test_dense_frames_with_header_like_payloads(ws, oracle, fake):
+    """Many small frames (the decoder's dense pass: sub-block chases from
+    speculated entries) whose wire payload bytes are themselves chains of
+    plausible client headers, so that speculated entries land inside payloads
+    and the sequential repair of the dense pass runs. GPU vs oracle: bytes,
+    count, descriptors."""
+    rng = streams.SplitMix(0xDE5E + fake)
+    out = bytearray()
+    while len(out) < (3 << 20):
+        plen = 120 + rng.below(400)
+        key = rng.bytes(4)
+        if fake == 0:
+            wire = rng.bytes(plen)
+        else:
+            # fake 7-byte frames (FIN binary, masked, 1-byte payload) or, for
+            # fake == 2, fake 126-form frames that jump within the segment
+            unit = (bytes([0x82, 0x81]) + rng.bytes(5)) if fake == 1 else \
+                (bytes([0x82, 0xFE, 0x00, 0x40]) + rng.bytes(4) + rng.bytes(64))
+            off = rng.below(len(unit))
+            wire = (rng.bytes(off) + unit * (plen // len(unit) + 2))[:plen]
+        out += streams.header(0x82, plen, key, None) + wire
+    src = bytes(out)
+    view, _ = dev_bytes(src)
+    dec = ws.frame_decoder()
+    ob = np.frombuffer(src, np.uint8).copy()
+    ofr, carry, on = oracle.decode_stream(ob)
+    r = dec.decode(view, cap=on + 2)
+    assert r.nframes == on
+    assert host(view) == ob.tobytes()
+    assert frames_list(r.frames(), True) == frames_list(ofr, True)
+    assert carry_list(dec.carry()) == carry_list(carry)
+
+
 # --------------------------------------------------------------------------- indexed
 def test_indexed_matches_golden(ws):
     g = load_golden("streams.json")["cases"]["lengths"]

@@ -58,7 +58,6 @@
 namespace {
 
 constexpr uint64_t NONE = ~0ull;
-constexpr uint32_t FCAP = 512;        // frame-list entries per pass
 constexpr uint32_t PAD = 32;          // LDS bytes after the segment (5-dword header reads)
 // Headers a speculative entry's chain must pass, by the entry's length form:
 // a false 127-form header needs 0xFF/0x7F plus an 8-byte length below 2^46
@@ -91,6 +90,11 @@ struct geom {
   // threads, 16-byte chunks per thread, waves per SIMD the decode kernel must
   // fit (register budget 512 / WPE)
   static constexpr uint32_t NT = NT_, CH = CH_, SEG = NT_ * CH_ * 16, WPE = WPE_;
+  // frame-list entries per pass (one per thread: the dense pass compacts them
+  // one per thread); prologue lists overlaying the frame list
+  static constexpr uint32_t FCAP = NT_, SCAP = NT_ * 2, UCAP = NT_ * 2;
+  // dense pass: sub-blocks (four per wave), their bytes and list sections
+  static constexpr uint32_t NSB = NT_ / 16, SB = SEG / NSB, SECT = FCAP / NSB;
 };
 using G_PROD = geom<1024, 8, 4>;  // 128 KiB segments, 16 waves, one workgroup per CU (default)
 using G_PROD2 = geom<512, 8, 4>;  // 64 KiB segments, 8 waves, two workgroups per CU (XYWS_OPT_WG512)
@@ -99,9 +103,6 @@ using G_SMALL = geom<64, 1, 1>;   // 1 KiB segments, one wave (XYWS_OPT_SMALL_SE
 struct fent {
   uint32_t start, ps, end, kw;  // segment-relative, clamped to [0, 2^32-1]
 };
-// prologue lists (they overlay the frame list): survivors of a segment's scan
-// filter and survivors whose chain left the segment (u32 segment offsets)
-constexpr uint32_t SCAP = FCAP * sizeof(fent) / 8, UCAP = FCAP * sizeof(fent) / 8;
 
 struct cstate {
   uint64_t X;          // next frame start (absolute)
@@ -143,10 +144,10 @@ template <class G>
 struct __attribute__((aligned(16))) lds_t {
   uint8_t seg[G::SEG + PAD];
   union {
-    fent fl[FCAP];
-    struct {
-      uint32_t sl[SCAP];
-      uint32_t ul[UCAP];
+    fent fl[G::FCAP];
+    struct {  // prologue: survivors of a segment's scan filter, and those whose chain left the segment
+      uint32_t sl[G::SCAP];
+      uint32_t ul[G::UCAP];
     };
   };
   cstate S;
@@ -157,6 +158,11 @@ struct __attribute__((aligned(16))) lds_t {
   // wave 0 after each chase pass: ROW_FAST (one key word for the whole row,
   // rk), ROW_SKIP (nothing to store) or the entry to start the walk from
   uint2 rt[G::SEG / 1024];  // (class or entry, key word)
+  // dense pass, per sub-block: speculated entry, frames, exit, last frame
+  // (start, payload start, key, key word)
+  uint32_t dent[G::NSB], dcnt[G::NSB], dexit[G::NSB], doff[G::NSB];
+  uint4 dlast[G::NSB];
+  uint32_t dense;  // frames of the previous pass (the dense pass is tried after a dense one)
 };
 
 // ---------------------------------------------------------------- small helpers
@@ -171,9 +177,9 @@ XYWS_DEV uint32_t flag_load(const uint32_t* p) {
 }
 XYWS_DEV bool stats_on(const run_params& P) { return (P.opts & XYWS_OPT_STATS) != 0; }
 enum { ST_RUNS = 0, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRAMES,
-       ST_P_WIN, ST_P_CAND, ST_P_UND, ST_P_TCOMP, ST_P_TCHECK, ST_P_TRES,
+       ST_P_WIN, ST_P_CAND, ST_P_UND, ST_P_TCOMP, ST_P_TCHECK, ST_P_TRES, ST_D_TENT, ST_D_TCHASE,
        ST_T_PRO = 16, ST_T_MAIN, ST_T_WAIT, ST_T_FILL, ST_T_CHASE, ST_T_XOR, ST_T_TAIL, ST_T_PF, ST_T_CP,
-       ST_P_FILL, ST_P_SCAN, ST_P_PUB };
+       ST_P_FILL, ST_P_SCAN, ST_P_PUB, ST_D_NOENT, ST_D_CHASE, ST_D_MISMATCH, ST_D_OVF };
 XYWS_DEV void stat_add(const run_params& P, uint32_t i, uint64_t v) {
   if (stats_on(P)) atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + i, (unsigned long long)v);
 }
@@ -305,6 +311,35 @@ XYWS_DEV uint32_t cand_nibble(uint32_t w, uint32_t wn, bool unmasked) {
   return ((c >> 7) & 1u) | ((c >> 14) & 2u) | ((c >> 21) & 4u) | ((c >> 28) & 8u);
 }
 
+// Candidate bits of the 16 positions of chunk a (bit t: position a + t).
+template <class G>
+XYWS_DEV uint32_t chunk_candidates(const run_params& P, const lds_t<G>& L, uint32_t a, bool unm) {
+  const u32x4 v = *reinterpret_cast<const u32x4*>(L.seg + a);
+  const uint32_t w4 = *reinterpret_cast<const uint32_t*>(L.seg + a + 16);
+  uint32_t bits = cand_nibble(v.x, v.y, unm) | (cand_nibble(v.y, v.z, unm) << 4) |
+                  (cand_nibble(v.z, v.w, unm) << 8) | (cand_nibble(v.w, w4, unm) << 12);
+  // headers straddling the segment end are left to the next segment's scan
+  if (a + 16 + 1 > G::SEG) bits &= (1u << (G::SEG - XYWS_MAX_FRAME_HEADER_SIZE - a + 1)) - 1u;
+  return bits;
+}
+
+// Candidate bits of the 4 positions of dword w (wn: the next dword) at bits
+// 7, 15, 23, 31: the cand_nibble test with fewer operations.
+XYWS_DEV uint32_t cand_bytes(uint32_t w, uint32_t wn, bool unmasked) {
+  const uint32_t b1s = __builtin_amdgcn_alignbyte(wn, w, 1);               // byte t = byte t+1
+  const uint32_t rsv = ((w & 0x74747474u) + 0x7F7F7F7Fu);                    // RSV or opcode bit 2
+  const uint32_t b3 = (w << 7) & (w << 6);                                   // opcode & 3 == 3
+  const uint32_t ctl = (w << 4) & ~w;                                        // control without FIN
+  const uint32_t m = unmasked ? ~b1s : b1s;
+  return m & ~(rsv | b3 | ctl) & 0x80808080u;
+}
+
+// First byte pair of a client header (cand_nibble for one position).
+XYWS_DEV bool cand_pair(uint32_t b0, uint32_t b1, bool unm) {
+  return (b0 & 0x74u) == 0 && (b0 & 3u) != 3u && !((b0 & 0x08u) && !(b0 & 0x80u)) &&
+         ((b1 >> 7) != 0) != unm;
+}
+
 // State before the first byte of the batch, from the carry snapshot; cnt =
 // frames it completes (the carried-header frame).
 XYWS_DEV cstate initial_state(const run_params& P, const xyws_carry* c, uint64_t& cnt) {
@@ -398,8 +433,41 @@ XYWS_DEV u32x4 chunk_xor(const lds_t<G>& L, uint32_t nfl, uint32_t g, uint32_t a
   return w;
 }
 
+// 32-bit parse of the header at segment offset x whose 14 bytes are in LDS:
+// header length, payload length, key (wire order) and the first two bytes.
+// False for a payload length of 2^31 or more (left to the 64-bit parse).
+template <class G>
+XYWS_DEV bool parse_rel(const lds_t<G>& L, uint32_t x, uint32_t& hl, uint32_t& plen, uint32_t& key, uint32_t& b01) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(L.seg + (x & ~3u));
+  const uint32_t sh = x & 3u, r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+  const uint32_t w0 = __builtin_amdgcn_alignbyte(r1, r0, sh), w1 = __builtin_amdgcn_alignbyte(r2, r1, sh);
+  b01 = w0 & 0xFFFFu;
+  const uint32_t b1 = (w0 >> 8) & 0xFFu, l7 = b1 & 0x7Fu, msk = b1 >> 7;
+  uint32_t ext;
+  if (l7 < 126) {
+    plen = l7; ext = 0;
+  } else if (l7 == 126) {
+    plen = ((w0 >> 8) & 0xFF00u) | (w0 >> 24); ext = 2;
+  } else {
+    const uint32_t w2 = __builtin_amdgcn_alignbyte(r3, r2, sh);
+    const uint32_t hi32 = __builtin_amdgcn_alignbyte(w1, w0, 2);  // bytes 2..5
+    const uint32_t lo32 = __builtin_amdgcn_alignbyte(w2, w1, 2);  // bytes 6..9
+    if (hi32 != 0u || (lo32 & 0x80u)) return false;
+    plen = __builtin_bswap32(lo32); ext = 8;
+  }
+  hl = 2 + ext + 4 * msk;
+  key = 0;
+  if (msk) {
+    if (ext == 0) key = __builtin_amdgcn_alignbyte(w1, w0, 2);
+    else if (ext == 2) key = w1;
+    else key = __builtin_amdgcn_alignbyte(__builtin_amdgcn_alignbyte(r4, r3, sh),
+                                          __builtin_amdgcn_alignbyte(r3, r2, sh), 2);
+  }
+  return true;
+}
+
 // One pass of the chase over segment [ss, ss+SEG), lane 0: the frame covering
-// the pass start, then frames parsed from X, up to FCAP entries. Sets
+// the pass start, then frames parsed from X, up to G::FCAP entries. Sets
 // pass_hi: the chunks below it are final for this pass.
 template <class G>
 XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t lo_c, uint32_t keep) {
@@ -433,31 +501,10 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
       if (!(S.st & (S_PARTIAL | S_CUT)) && X0 >= ss && X0 < fstop) {
         const uint32_t st = (uint32_t)(fstop - ss);
         uint32_t x = (uint32_t)(X0 - ss), lx = 0, lps = 0, lkey = 0, lkw = 0, k = 0;
-        while (x < st && n < FCAP) {
-          const uint32_t* q = reinterpret_cast<const uint32_t*>(L.seg + (x & ~3u));
-          const uint32_t sh = x & 3u, r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
-          const uint32_t w0 = __builtin_amdgcn_alignbyte(r1, r0, sh), w1 = __builtin_amdgcn_alignbyte(r2, r1, sh);
-          const uint32_t b1 = (w0 >> 8) & 0xFFu, l7 = b1 & 0x7Fu, msk = b1 >> 7;
-          uint32_t plen, ext;
-          if (l7 < 126) {
-            plen = l7; ext = 0;
-          } else if (l7 == 126) {
-            plen = ((w0 >> 8) & 0xFF00u) | (w0 >> 24); ext = 2;
-          } else {
-            const uint32_t w2 = __builtin_amdgcn_alignbyte(r3, r2, sh);
-            const uint32_t hi32 = __builtin_amdgcn_alignbyte(w1, w0, 2);   // bytes 2..5
-            const uint32_t lo32 = __builtin_amdgcn_alignbyte(w2, w1, 2);   // bytes 6..9
-            if (hi32 != 0u || (lo32 & 0x80u)) break;                        // >= 2^31: general step
-            plen = __builtin_bswap32(lo32); ext = 8;
-          }
-          const uint32_t hl = 2 + ext + 4 * msk, ps = x + hl;
-          uint32_t key = 0;
-          if (msk) {
-            if (ext == 0) key = __builtin_amdgcn_alignbyte(w1, w0, 2);
-            else if (ext == 2) key = w1;
-            else key = __builtin_amdgcn_alignbyte(__builtin_amdgcn_alignbyte(r4, r3, sh),
-                                                  __builtin_amdgcn_alignbyte(r3, r2, sh), 2);
-          }
+        while (x < st && n < G::FCAP) {
+          uint32_t hl, plen, key, b01;
+          if (!parse_rel<G>(L, x, hl, plen, key, b01)) break;  // >= 2^31: general step
+          const uint32_t ps = x + hl;
           const uint32_t kw = rotr8(key, 0u - ps);  // aligned_key: ss is 16-byte aligned
           fent e;
           e.start = x; e.ps = ps; e.end = ps + plen; e.kw = kw;
@@ -481,7 +528,7 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
     }
     if (X >= P.hi || (S.st & (S_PARTIAL | S_CUT))) { end = true; break; }
     if (X >= lim) { done = true; break; }
-    if (X >= se || n >= FCAP) break;
+    if (X >= se || n >= G::FCAP) break;
     const hdr_info h = hdr_at(P, L, ss, X, lim);
     if (!h.hlen) {
       // incomplete: at the batch end (carry) or at the successor's write start
@@ -508,8 +555,219 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   L.tail += tail;
   L.S = S;
   L.nfl = n;
+  L.dense = n;
   const bool seg_done = S.X >= se || end || done;
   L.pass_hi = seg_done ? G::SEG : (uint32_t)((S.X - ss) & ~15ull);
+}
+
+// Dense pass (many small frames): the segment's chase split over NSB
+// sub-blocks of SB bytes, four per wave, chased at once. Sub-block 0 starts
+// from the exact state; sub-block b > 0 from its speculated entry, the
+// earliest position in its first 512 bytes whose next 4 headers (32-bit parse
+// in LDS) have client first bytes. Every chase starts exactly where the previous
+// sub-block's chase leaves the previous sub-block, or the pass is abandoned
+// (false, nothing of the chain state changed) and the serial chase runs: a
+// chain is determined by its start, so sub-block b's frames are exact once its
+// start is, by induction from sub-block 0. Entries go to per-sub-block sections
+// of the frame list and are compacted (one per thread). A last header that
+// does not fit the segment ends the pass (pass_hi) and the serial chase
+// continues it. Called only where no limit lies in the segment.
+template <class G>
+XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid, bool unm, bool past) {
+  constexpr uint32_t NSB = G::NSB, SB = G::SB, SECT = G::SECT, NONE32 = 0xFFFFFFFFu;
+  constexpr uint32_t STOP = G::SEG - XYWS_MAX_FRAME_HEADER_SIZE + 1;  // headers wholly in LDS start below
+  const uint32_t lane = tid & 63u, gl = lane & 15u, sb = (tid >> 6) * 4 + (lane >> 4);
+  const cstate S0 = L.S;
+  const uint32_t x0 = (uint32_t)(S0.X - ss);
+  const bool st_on = stats_on(P) && tid == 0;
+  uint64_t tq = st_on ? __builtin_amdgcn_s_memtime() : 0;
+  if (gl == 0) L.dent[sb] = sb == 0 ? x0 : NONE32;
+  __syncthreads();
+  if (st_on) tq = __builtin_amdgcn_s_memtime();
+  // 1. speculated entries: each lane of the 16-lane group takes WIN/16 bytes
+  if (sb > 0) {
+    constexpr uint32_t WIN = SB < 512 ? SB : 512, PER = WIN / 16;
+    auto qchain = [&](uint32_t p) -> bool {
+      uint32_t x = p;
+#pragma unroll 1
+      for (uint32_t h = 0; h < 4; h++) {
+        if (x >= STOP) return h >= 3;  // (one long hop out of the segment proves little)
+        uint32_t hl, plen, key, b01;
+        if (!parse_rel<G>(L, x, hl, plen, key, b01)) return false;
+        if (!cand_pair(b01 & 0xFFu, b01 >> 8, unm)) return false;
+        x += hl + plen;
+      }
+      return true;
+    };
+#pragma unroll 1
+    for (uint32_t c = 0; c < PER / 16; c++) {
+      const uint32_t a = sb * SB + gl * PER + c * 16;
+      uint32_t bits = chunk_candidates<G>(P, L, a, unm);
+      bool hit = false;
+      while (bits) {
+        const uint32_t t = __builtin_ctz(bits);
+        bits &= bits - 1;
+        if (qchain(a + t)) {
+          atomicMin(&L.dent[sb], a + t);
+          hit = true;
+          break;
+        }
+      }
+      if (hit) break;
+    }
+  }
+  __syncthreads();
+  if (st_on) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    stat_add(P, ST_D_TENT, t - tq);
+    tq = t;
+  }
+  // 2. one chase per sub-block (lane 0 of each 16-lane group)
+  if (gl == 0) {
+    uint32_t x = L.dent[sb], n = 0, lx = 0, lps = 0, lkey = 0, lkw = 0;
+    bool fail = x == NONE32;
+    const uint32_t end = (sb + 1) * SB;
+    while (!fail && x < end && x < STOP) {
+      uint32_t hl, plen, key, b01;
+      if (n >= SECT || !parse_rel<G>(L, x, hl, plen, key, b01)) { fail = true; break; }
+      const uint32_t ps = x + hl, kw = rotr8(key, 0u - ps);
+      fent e;
+      e.start = x; e.ps = ps; e.end = ps + plen; e.kw = kw;
+      L.fl[sb * SECT + n] = e;
+      n++;
+      lx = x; lps = ps; lkey = key; lkw = kw;
+      x = ps + plen;
+    }
+    // (a header starting at or past STOP ends the pass; only the last
+    // sub-block can reach it)
+    if (x < end && sb + 1 < NSB) fail = true;
+    L.dcnt[sb] = fail ? NONE32 : n;
+    L.dexit[sb] = x;
+    L.dlast[sb] = uint4{lx, lps, lkey, lkw};
+  }
+  __syncthreads();
+  if (st_on) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    stat_add(P, ST_D_TCHASE, t - tq);
+    tq = t;
+  }
+  // 3. validation and offsets (wave 0, one lane per sub-block)
+  const bool cover = !(S0.st & (S_NOCOV | S_PARTCARRY)) && S0.X > ss;
+  if (tid < 64) {
+    bool ok = true;
+    uint32_t c = 0;
+    if (lane < NSB) {
+      c = L.dcnt[lane];
+      if (c == NONE32) {
+        ok = false;
+        if (stats_on(P)) stat_add(P, L.dent[lane] == NONE32 ? ST_D_NOENT : ST_D_CHASE, 1);
+      } else if (lane > 0) {
+        // the previous chase's exit must be one of this chase's frame starts
+        // (usually the first; a false header just before a true one can land
+        // on it): the frames from there on are exact
+        const uint32_t xp = L.dexit[lane - 1];
+        uint32_t j = 0;
+        while (j < c && L.fl[lane * SECT + j].start < xp) j++;
+        ok = j < c && L.fl[lane * SECT + j].start == xp;
+        if (!ok && stats_on(P)) stat_add(P, ST_D_MISMATCH, 1);
+        L.dent[lane] = j;  // entries skipped
+        c -= j;
+      } else {
+        L.dent[0] = 0;
+      }
+      if (!ok) c = 0;
+    }
+    const bool all = __ballot(!ok) == 0;
+    // exclusive prefix of the counts over the lanes
+    uint32_t incl = c;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
+    }
+    const uint32_t total = __shfl(incl, 63) + (cover ? 1u : 0u);
+    if (lane < NSB) L.doff[lane] = (cover ? 1u : 0u) + incl - c;
+    if (lane == 0) L.ccnt = all && total <= G::FCAP ? total : NONE32;
+    if (lane == 0 && all && total > G::FCAP) stat_add(P, ST_D_OVF, 1);
+    if (!all && lane == 0) {
+      // a speculated entry was wrong (rare): walk the sub-blocks in order,
+      // re-chasing each one whose frames do not contain the exact exit of the
+      // previous one, from that exit; give up (serial chase) on overflow
+      uint32_t tot = cover ? 1u : 0u;
+      bool good = L.dcnt[0] != NONE32;
+      if (good) { L.dent[0] = 0; L.doff[0] = tot; tot += L.dcnt[0]; }
+      for (uint32_t b = 1; b < NSB && good; b++) {
+        const uint32_t xp = L.dexit[b - 1], cb = L.dcnt[b];
+        uint32_t j = 0;
+        if (cb != NONE32)
+          while (j < cb && L.fl[b * SECT + j].start < xp) j++;
+        if (cb == NONE32 || j >= cb || L.fl[b * SECT + j].start != xp) {
+          uint32_t x = xp, n = 0, lx = 0, lps = 0, lkey = 0, lkw = 0;
+          const uint32_t end = (b + 1) * SB;
+          while (x < end && x < STOP) {
+            uint32_t hl, plen, key, b01;
+            if (n >= SECT || !parse_rel<G>(L, x, hl, plen, key, b01)) { good = false; break; }
+            const uint32_t ps = x + hl, kw = rotr8(key, 0u - ps);
+            fent e;
+            e.start = x; e.ps = ps; e.end = ps + plen; e.kw = kw;
+            L.fl[b * SECT + n] = e;
+            n++;
+            lx = x; lps = ps; lkey = key; lkw = kw;
+            x = ps + plen;
+          }
+          if (x < end && b + 1 < NSB) good = false;
+          L.dcnt[b] = n;
+          L.dexit[b] = x;
+          if (n) L.dlast[b] = uint4{lx, lps, lkey, lkw};
+          j = 0;
+        }
+        L.dent[b] = j;
+        L.doff[b] = tot;
+        tot += L.dcnt[b] - j;
+      }
+      L.ccnt = good && tot <= G::FCAP ? tot : NONE32;
+    }
+  }
+  __syncthreads();
+  const uint32_t total = L.ccnt;
+  if (total == NONE32) return false;
+  // 4. compaction (each thread moves at most one entry) and the chain state
+  {
+    const uint32_t s = tid / SECT, j = tid % SECT, skip = L.dent[s];
+    const bool mv = j >= skip && j < L.dcnt[s];
+    fent e;
+    if (mv) e = L.fl[tid];
+    __syncthreads();
+    if (mv) L.fl[L.doff[s] + j - skip] = e;
+  }
+  if (tid == 0) {
+    if (cover) {
+      fent e;
+      e.start = 0;
+      e.ps = clamp_rel(S0.cov_ps, ss);
+      e.end = clamp_rel(S0.X, ss);
+      e.kw = S0.cov_kw;
+      L.fl[0] = e;
+    }
+    uint32_t last = NSB - 1;  // the last sub-block with frames
+    while (last > 0 && L.dcnt[last] == L.dent[last]) last--;
+    const uint4 f = L.dlast[last];
+    const uint32_t xe = L.dexit[NSB - 1];
+    const uint32_t frames = total - (cover ? 1u : 0u);
+    if (frames) {
+      cstate S;
+      S.cov_start = ss + f.x; S.cov_ps = ss + f.y; S.X = ss + xe;
+      S.cov_key = f.z; S.cov_kw = f.w; S.st = 0; S.pad = 0;
+      L.S = S;
+    }
+    if (past) L.tail += frames; else L.cnt += frames;
+    L.nfl = total;
+    L.dense = total;
+    stat_add(P, ST_SEGS, 1);
+    L.pass_hi = xe >= G::SEG ? G::SEG : (xe & ~15u);
+  }
+  __syncthreads();
+  return true;
 }
 
 // Row table of one pass (wave 0, after lane 0's chase_pass; rows r = lane,
@@ -637,6 +895,7 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
     // (issuing each chunk's next load right after its LDS write made hipcc wait
     // for the new loads inside the fill: the prefetch goes after the barrier)
     if (pf) io.issue(P, nx, tid, known ? wlim : NONE);
+    XYWS_STAMP(acc_pf);
     const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss);
     uint32_t lo_c = 0, keep = 0;
     for (;;) {
@@ -644,11 +903,22 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
       const uint32_t wl_r = wl > ss ? (wl - ss < G::SEG ? (uint32_t)(wl - ss) : G::SEG) : 0u;
       const uint32_t wh_r = whi > ss ? (whi - ss < G::SEG ? (uint32_t)(whi - ss) : G::SEG) : 0u;
       const bool any = stores && !(P.opts & XYWS_OPT_NO_STORE) && wl_r < wh_r;
+      // the dense pass where the previous pass found many frames and no limit
+      // lies in this segment (the serial chase below otherwise, or after it)
+      bool dense = false;
+      if (lo_c == 0 && keep == 0 && L.dense >= 2 * G::NSB) {
+        const cstate S0 = L.S;
+        const bool kn = L.known != 0, pst = L.past != 0;
+        const uint64_t se14 = ss + G::SEG + XYWS_MAX_FRAME_HEADER_SIZE;
+        if (!(S0.st & (S_PARTIAL | S_CUT)) && S0.X >= ss && S0.X < ss + G::SB && P.hi >= se14 &&
+            (!kn || (L.Wn >= se14 && (pst || L.hn >= se14))))
+          dense = dense_pass<G>(P, L, ss, tid, (P.opts & XYWS_OPT_UNMASKED_HINT) != 0, pst);
+      }
       if (tid < 64) {
         // lane 0 chases; then wave 0 classifies the rows (the other waves wait
         // at the barrier with their prefetch in flight: work here is hidden,
         // work in the store loop below is not)
-        if (tid == 0) chase_pass(P, L, ss, lo_c, keep);
+        if (tid == 0 && !dense) chase_pass(P, L, ss, lo_c, keep);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -812,35 +1082,6 @@ XYWS_DEV uint32_t chain_plausible(const run_params& P, const lds_t<G>& L, uint64
   return 1u;
 }
 
-// Candidate bits of the 16 positions of chunk a (bit t: position a + t).
-template <class G>
-XYWS_DEV uint32_t chunk_candidates(const run_params& P, const lds_t<G>& L, uint32_t a, bool unm) {
-  const u32x4 v = *reinterpret_cast<const u32x4*>(L.seg + a);
-  const uint32_t w4 = *reinterpret_cast<const uint32_t*>(L.seg + a + 16);
-  uint32_t bits = cand_nibble(v.x, v.y, unm) | (cand_nibble(v.y, v.z, unm) << 4) |
-                  (cand_nibble(v.z, v.w, unm) << 8) | (cand_nibble(v.w, w4, unm) << 12);
-  // headers straddling the segment end are left to the next segment's scan
-  if (a + 16 + 1 > G::SEG) bits &= (1u << (G::SEG - XYWS_MAX_FRAME_HEADER_SIZE - a + 1)) - 1u;
-  return bits;
-}
-
-// Candidate bits of the 4 positions of dword w (wn: the next dword) at bits
-// 7, 15, 23, 31: the cand_nibble test with fewer operations.
-XYWS_DEV uint32_t cand_bytes(uint32_t w, uint32_t wn, bool unmasked) {
-  const uint32_t b1s = __builtin_amdgcn_alignbyte(wn, w, 1);               // byte t = byte t+1
-  const uint32_t rsv = ((w & 0x74747474u) + 0x7F7F7F7Fu);                    // RSV or opcode bit 2
-  const uint32_t b3 = (w << 7) & (w << 6);                                   // opcode & 3 == 3
-  const uint32_t ctl = (w << 4) & ~w;                                        // control without FIN
-  const uint32_t m = unmasked ? ~b1s : b1s;
-  return m & ~(rsv | b3 | ctl) & 0x80808080u;
-}
-
-// First byte pair of a client header (cand_nibble for one position).
-XYWS_DEV bool cand_pair(uint32_t b0, uint32_t b1, bool unm) {
-  return (b0 & 0x74u) == 0 && (b0 & 3u) != 3u && !((b0 & 0x08u) && !(b0 & 0x80u)) &&
-         ((b1 >> 7) != 0) != unm;
-}
-
 // Second-level filter for the candidate at segment offset p (cheap, from LDS):
 // false only when the header after it (7-bit or 126 form) lies in the segment
 // and the batch and fails cand_pair, i.e. when its chain is certainly
@@ -897,7 +1138,7 @@ XYWS_DEV void scan_segment(const run_params& P, lds_t<G>& L, uint64_t ss, uint32
   auto survivor = [&](uint32_t pos) {
     if (second_hop_ok<G>(P, L, ss, pos, unm)) {
       const uint32_t slot = atomicAdd(&L.ccnt, 1u);
-      if (slot < SCAP) L.sl[slot] = pos;
+      if (slot < G::SCAP) L.sl[slot] = pos;
     }
   };
   // survivors' chains in LDS, one per lane; chains leaving the segment are
@@ -909,7 +1150,7 @@ XYWS_DEV void scan_segment(const run_params& P, lds_t<G>& L, uint64_t ss, uint32
       const uint64_t t = __builtin_amdgcn_s_memtime();
       a_filt += t - tq; tq = t; nwin++; nsurv += n;
     }
-    if (n > SCAP) {
+    if (n > G::SCAP) {
       if (tid == 0) L.ovf = 1;
     } else {
       // (i is opaque to the compiler: a hoisted, spilled &L.sl[tid] would be
@@ -924,7 +1165,7 @@ XYWS_DEV void scan_segment(const run_params& P, lds_t<G>& L, uint64_t ss, uint32
           atomicMin(&L.best, pos);
         } else if (r == 2u) {
           const uint32_t u = atomicAdd(&L.ucnt, 1u);
-          if (u < UCAP) L.ul[u] = pos;
+          if (u < G::UCAP) L.ul[u] = pos;
           else L.ovf = 1;
         }
       }
@@ -1136,6 +1377,8 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
       __hip_atomic_store(P.flags + run, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       L.S = S;
       L.cnt = hc;
+      // dense-pass hint for the first segment: the entry's frame is small
+      L.dense = (h != NONE && S.X - S.cov_start < 1024) ? G::FCAP : 0;
       L.aux2 = h == NONE ? NONE : W;
       stat_add(P, ST_RUNS, 1);
       if (h == NONE) stat_add(P, ST_NONE, 1);
@@ -1153,6 +1396,7 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
   }
   if (tid == 0) {
     L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.first_after = NONE;
+    if (run == 0) L.dense = 0;
     L.known = rng_end == NONE;
     L.hn = NONE; L.Wn = NONE; L.succ = P.nruns;
   }
@@ -1296,7 +1540,7 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
         L.hn = st_load(rs + R_HN);
         L.Wn = st_load(rs + R_WN);
         L.succ = st_load(rs + R_OK) >> 32;
-        L.known = 1; L.cnt = 0; L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0;
+        L.known = 1; L.cnt = 0; L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.dense = 0;
         L.first_after = NONE;
         L.best = 0;
       }
@@ -1317,7 +1561,7 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
       L.S = L.B;
       L.S.st &= ~S_CUT;
       L.hn = hn; L.Wn = Wn; L.succ = succ;
-      L.known = 1; L.cnt = 0; L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0;
+      L.known = 1; L.cnt = 0; L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.dense = 0;
       L.first_after = NONE;
       L.repaired = 1;
     }
