@@ -29,9 +29,19 @@ rec = np.frombuffer(tab.numpy().tobytes(), dtype=np.dtype(
 starts = rec["off"].astype(np.int64)
 sset = set(starts.tolist())
 dec = ws.frame_decoder()
-dec.opts |= 0x100 | xo
-dec.decode(buf, cap=0, count=False, carry=False)
-torch.cuda.synchronize()
+dec.opts |= xo
+# the bench decodes the same buffer repeatedly (payloads alternate masked /
+# unmasked); find the first decode with a bad boundary
+NONE = (1 << 64) - 1
+for it in range(int(os.environ.get("ITERS", "12"))):
+    dec.opts |= 0x100
+    dec.decode(buf, cap=0, count=False, carry=False)
+    torch.cuda.synchronize()
+    st = (C.c_uint64 * 32)()
+    dec.ctx.L.xyws_debug_stats(dec.ctx.h, st)
+    print("decode", it, "bad", st[2], "repairs", st[3])
+    if st[2]:
+        break
 out = (C.c_uint64 * 32)()
 dec.ctx.L.xyws_debug_stats(dec.ctx.h, out)
 print("stats", list(out)[:16])
@@ -52,6 +62,11 @@ for i in range(nr):
               f"hn_true={hn in sset} first_after={first} first_true={first in sset} "
               f"frame_before_h: off={starts[j] if j >= 0 else None} plen={rec['plen'][j] if j >= 0 else None}")
 buf2, _ = bench.build_batch(torch, T, "c4", 0, 1)
+if it % 2 == 1:  # the decode that failed saw the payloads unmasked once more
+    dec2 = ws.frame_decoder()
+    for _ in range(it):
+        dec2.decode(buf2, cap=0, count=False, carry=False)
+    torch.cuda.synchronize()
 for i in range(nr):
     h = int(r[i, 0])
     if h != (1 << 64) - 1 and h not in sset:

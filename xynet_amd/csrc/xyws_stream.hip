@@ -1068,10 +1068,13 @@ XYWS_DEV uint32_t chain_plausible(const run_params& P, const lds_t<G>& L, uint64
   uint64_t x = q;
   uint32_t need = KHDR_7;
   for (uint32_t i = 0; i < need; i++) {
-    if (x >= P.hi) return i > 0;  // the chain ends with the batch
+    // a chain that ends with the batch counts after two verified headers (one
+    // header whose length jumps past the batch end proves nothing: random
+    // bytes 0xFF 0x00 0x00 ... pass as a 64-bit length below 2^46 often enough)
+    if (x >= P.hi) return i >= 2;
     if (!mem && x - ss + XYWS_MAX_FRAME_HEADER_SIZE > G::SEG) return 2u;  // (x >= ss always)
     const hdr_info h = hdr_at(P, L, ss, x, NONE);
-    if (!h.hlen) return i > 0;    // a header cut by the batch end
+    if (!h.hlen) return i >= 2;   // a header cut by the batch end
     if (!plausible(h, unm)) return 0u;
     if (i == 0) {
       const uint32_t ext = h.hlen - 2 - ((h.status & XYWS_ST_UNMASKED) ? 0u : 4u);
