@@ -61,7 +61,9 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    path = lib_path()
+    # XYWS_LIB: an alternative in-tree build of the same library (A/B timing
+    # of compile-time variants; scripts/exp_variants.sh)
+    path = os.environ.get("XYWS_LIB") or lib_path()
     if not os.path.exists(path):
         raise XywsError(-2, f"{path} missing: build it with `python -m xynet_amd.build`")
     L = C.CDLL(path)

@@ -1442,14 +1442,27 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
     const uint32_t lane = tid & 63u, wave = tid >> 6;
     uint64_t carry = 0;
     uint32_t bad = 0, last = 0;
+    bool has = false;
+    cstate fsl;  // final state of this thread's last visible run
     for (uint32_t t0 = 0; t0 < P.nruns; t0 += G::NT) {
       const uint32_t r = t0 + tid;
       const uint64_t* rec = P.rec + (uint64_t)r * R_WORDS;
-      const uint64_t h = r < P.nruns ? st_load(rec + R_H) : NONE;
+      // every word this pass needs is loaded at once (one memory round trip
+      // instead of three dependent ones; the final state of the last visible
+      // run comes from its own thread)
+      uint64_t h = NONE, cw = 0, okw = 1;
+      cstate fs;
+      if (r < P.nruns) {
+        h = st_load(rec + R_H);
+        cw = st_load(rec + R_CNT);
+        okw = st_load(rec + R_OK);
+        fs = get_state(rec + R_F0);
+      }
       const bool vis = r < P.nruns && (r == 0 || h != NONE);
-      const uint64_t cnt = vis ? st_load(rec + R_CNT) : 0;
-      if (vis && !(st_load(rec + R_OK) & 1u)) bad = 1;
+      const uint64_t cnt = vis ? cw : 0;
+      if (vis && !(okw & 1u)) bad = 1;
       if (vis) last = r;
+      if (vis) { fsl = fs; has = true; }
       uint64_t x = cnt;  // wave inclusive scan
 #pragma unroll
       for (uint32_t o = 1; o < 64; o <<= 1) {
@@ -1480,10 +1493,8 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
     if (last) atomicMax(reinterpret_cast<unsigned long long*>(&L.aux1), (unsigned long long)last);
     __syncthreads();
     if (!any_bad) {
-      if (tid == 0) {
-        L.aux2 = carry;
-        L.S = get_state(P.rec + L.aux1 * R_WORDS + R_F0);
-      }
+      if (tid == 0) L.aux2 = carry;
+      if (has && last == L.aux1) L.S = fsl;
       __syncthreads();
     }
     if (any_bad) stat_add(P, ST_BAD, 0);
