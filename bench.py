@@ -268,13 +268,13 @@ def main():
                  "cyc_scan_check", "cyc_scan_resolve", "cyc_dense_entry", "cyc_dense_chase", "cyc_prologue", "cyc_main", "cyc_wait",
                  "cyc_fill", "cyc_chase_sync", "cyc_xor", "cyc_tail", "cyc_prefetch_issue", "cyc_chase_pass",
                  "cyc_pro_fill", "cyc_pro_scan", "cyc_pro_publish", "dense_no_entry", "dense_chase_fail",
-                 "dense_mismatch", "dense_overflow"]
+                 "dense_mismatch", "dense_overflow", "giveups", "bridges", "-"]
         for _ in range(2):
-            dec.opts |= 0x100
+            dec.opts |= _lib.OPT_STATS
             dec.decode(buf, cap=0, count=False, carry=False)
-            dec.opts &= ~0x100
-            out = (C.c_uint64 * 32)()
-            dec.ctx.L.xyws_debug_stats(dec.ctx.h, out)
+            dec.opts &= ~_lib.OPT_STATS
+            out = (C.c_uint64 * _lib.NSTATS)()
+            dec.ctx.L.xyws_debug_stats(dec.ctx.h, C.c_void_p(stream.cuda_stream), out)
         st = {k: v for k, v in zip(names, list(out)) if k != "-"}
         nrun = max(1, st["runs"] + 1)
         for k in list(st):

@@ -138,6 +138,15 @@ class Oracle:
                                         C.byref(cout), frames, n_est)
         return [frames[i] for i in range(min(n, n_est))], cout, n
 
+    def decode_stream_raw(self, buf: np.ndarray, cap, carry_in=None):
+        """decode_stream with the descriptors as one uint8 array (cap * 32 B)."""
+        raw = np.zeros(max(cap, 1) * 32, np.uint8)
+        cout = Carry()
+        n = self.L.oracle_decode_stream(_ptr(buf), buf.size,
+                                        C.byref(carry_in) if carry_in is not None else None,
+                                        C.byref(cout), _ptr(raw), cap)
+        return raw[: min(n, cap) * 32], cout, n
+
     def decode_indexed(self, buf: np.ndarray, starts):
         st = np.ascontiguousarray(np.asarray(starts, dtype=np.uint64))
         frames = (Frame * max(1, st.size))()
@@ -146,6 +155,17 @@ class Oracle:
 
     def digest(self, buf: np.ndarray) -> int:
         return self.L.oracle_digest(_ptr(buf), buf.size)
+
+    def frames_digest(self, raw: np.ndarray) -> int:
+        """Digest of a descriptor table (xyws_frame records as raw bytes): the
+        fields the reference defines (offsets, length, key, flags, header
+        length) and the PAYLOAD_INCOMPLETE status bit; the informational RFC
+        status bits (which the reference does not compute) and the reserved
+        byte are masked out."""
+        a = np.ascontiguousarray(raw, dtype=np.uint8).reshape(-1, 32).copy()
+        a[:, 30] &= 1
+        a[:, 31] = 0
+        return self.digest(a.reshape(-1))
 
     def fill_uniform(self, nframes, plen, b0, seed) -> np.ndarray:
         H = 2 + (0 if plen < 126 else (2 if plen <= 0xFFFF else 8)) + 4
@@ -256,6 +276,13 @@ class Reference:
                                      C.byref(carry_in) if carry_in is not None else None,
                                      C.byref(cout), frames, n_est)
         return [frames[i] for i in range(min(n, n_est))], cout, n
+
+    def decode_stream_raw(self, buf, cap):
+        """decode_stream with the descriptors as one uint8 array (cap * 32 B)."""
+        raw = np.zeros(max(cap, 1) * 32, np.uint8)
+        cout = Carry()
+        n = self.L.ref_decode_stream(_ptr(buf), buf.size, None, C.byref(cout), _ptr(raw), cap)
+        return raw[: min(n, cap) * 32], cout, n
 
     def decode_batch_mt(self, buf, threads):
         return self.L.ref_decode_batch_mt(_ptr(buf), buf.size, threads)

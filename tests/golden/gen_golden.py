@@ -31,7 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, HERE)
 
-from oracle.oracle import Oracle, Reference, Carry, NPOS  # noqa: E402
+from oracle.oracle import Oracle, Reference, Carry, Frame, NPOS  # noqa: E402
 import streams  # noqa: E402
 
 FIN, MASK, PING = 0x10, 0x20, 0x09
@@ -203,11 +203,17 @@ def gen_configs(ref, orc, only=None):
             rec = dict(kind=kind, target=p, seed=seed, nframes=nf)
         rec["size"] = int(buf.size)
         rec["in_digest"] = orc.digest(buf)
-        frames, cout, nd = ref.decode_stream(buf, cap=16)
+        nmax = n if n is not None else nf
+        raw, cout, nd = ref.decode_stream_raw(buf, nmax)
+        assert nd == nmax, (name, nd, nmax)
         rec["decoded_frames"] = nd
         rec["out_digest"] = orc.digest(buf)
         rec["carry"] = carry_json(cout)
-        rec["first_frames"] = frames_json(frames[:4])
+        first = (Frame * 4).from_buffer_copy(raw[:4 * 32].tobytes())
+        rec["first_frames"] = frames_json(list(first))
+        # the whole descriptor table the reference produced (what a
+        # websocket_recv_data caller consumes, websocket.h:110-134)
+        rec["frames_digest"] = orc.frames_digest(raw)
         out[name] = rec
         del buf
         print(f"  {name}: {rec['size']} B, {nd} frames, {time.time() - t0:.1f}s")
@@ -217,6 +223,9 @@ def gen_configs(ref, orc, only=None):
 def main():
     ref = Reference("O2")
     orc = Oracle()
+    if "--configs" in sys.argv:  # only configs.json
+        gen_configs(ref, orc)
+        return
     gen_frame_header(ref)
     gen_parse_corpus(ref)
     gen_unmask(ref)

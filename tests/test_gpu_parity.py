@@ -17,7 +17,10 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-MODES = {"fused": {}, "serial": {"serial": True}, "runs1k": {"small_segments": True}}
+OPT_TEST_GIVEUP = 0x100000  # xyws_stream.h: odd runs give up on their successor (finish bridges them)
+MODES = {"fused": {}, "serial": {"serial": True}, "runs1k": {"small_segments": True},
+         "giveup": {"opts": OPT_TEST_GIVEUP},
+         "runs1k_giveup": {"small_segments": True, "opts": OPT_TEST_GIVEUP}}
 
 
 @pytest.fixture(scope="module")
@@ -134,7 +137,7 @@ def test_stream_split_with_carry(ws, name, mode):
         assert [[x[0] + k, x[1] + k] + x[2:] for x in fb] == g["frames"][s["n1"]:]
 
 
-@pytest.mark.parametrize("mode", ["fused", "runs1k"])
+@pytest.mark.parametrize("mode", ["fused", "runs1k", "runs1k_giveup"])
 def test_fuzz_random_streams_vs_oracle(ws, oracle, mode):
     """Random frame soups + random cut points, GPU vs oracle."""
     rng = streams.SplitMix(0xF022)
@@ -269,19 +272,75 @@ def dev_digest(buf):
     return int(out[0].item()) & ((1 << 64) - 1)
 
 
-@pytest.mark.parametrize("name,mode", [(n, "fused") for n in [
+CONFIG_CASES = ([(n, "fused") for n in [
     "t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m", "c1_text_4k", "c2_bin_256", "c3_bin_64k",
-    "c4_mixed", "c5_shard0", "c5_shard7"]] + [(n, "runs1k") for n in [
-    "t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m"]])
-def test_config_batches(ws, name, mode):
+    "c4_mixed", "c5_shard0", "c5_shard7"]] +
+    [(n, "runs1k") for n in ["t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m"]] +
+    [(n, "giveup") for n in ["t_mixed_8m", "c1_text_4k", "c2_bin_256", "c4_mixed", "c5_shard3"]] +
+    [(n, "runs1k_giveup") for n in ["t_bin_256_x4096", "t_mixed_8m"]])
+
+
+def frames_digest(oracle, r, n):
+    return oracle.frames_digest(r.frames_t[: n * 32].cpu().numpy())
+
+
+@pytest.mark.parametrize("name,mode", CONFIG_CASES)
+def test_config_batches(ws, oracle, name, mode):
+    """Full bench batches: output bytes, count, carry and the WHOLE descriptor
+    table (every frame's offsets, length, key, flags, header length) against
+    the reference's (tests/golden/configs.json, from oracle/_ref)."""
     buf, c = tools_batch(name)
     assert dev_digest(buf) == c["in_digest"], "device generator disagrees with the host spec"
     dec = ws.frame_decoder(**MODES[mode])
-    r = dec.decode(buf, cap=16)
-    assert r.nframes == c["decoded_frames"]
+    n = c["decoded_frames"]
+    r = dec.decode(buf, cap=n)
+    assert r.nframes == n
     assert dev_digest(buf) == c["out_digest"]
     assert carry_list(dec.carry()) == c["carry"]
     assert frames_list(r.frames()[:4]) == c["first_frames"]
+    assert frames_digest(oracle, r, n) == c["frames_digest"]
     assert dec.ctx.last_device_error() == 0
-    del buf
+    del buf, r
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("same_ctx", [False, True])
+def test_concurrent_decodes_on_two_streams(ws, oracle, same_ctx):
+    """Two full-grid decodes at once on two streams (two contexts, or one
+    context: per-stream scratch): together they want twice the CUs, so runs
+    find successors whose workgroups have not started, give up on them, and
+    k_stream_finish bridges the gaps. Both outputs must be the reference's."""
+    names = ["c5_shard0", "c5_shard1"]
+    batches = [tools_batch(n) for n in names]
+    torch.cuda.synchronize()
+    streams_ = [torch.cuda.Stream() for _ in names]
+    ctx0 = ws.Context(0)
+    ctxs = [ctx0, ctx0] if same_ctx else [ctx0, ws.Context(0)]
+    decs = [ws.frame_decoder(ctx=c) for c in ctxs]
+    results = []
+    for rep in range(3):  # odd number of decodes: every payload ends unmasked
+        res = []
+        for (buf, c), st, dec in zip(batches, streams_, decs):
+            with torch.cuda.stream(st):
+                dec.reset()
+                res.append(dec.decode(buf, cap=c["decoded_frames"]))
+        results = res
+    torch.cuda.synchronize()
+    for (buf, c), r, dec in zip(batches, results, decs):
+        assert r.nframes == c["decoded_frames"]
+        assert dev_digest(buf) == c["out_digest"]
+        assert frames_digest(oracle, r, c["decoded_frames"]) == c["frames_digest"]
+        assert carry_list(dec.carry()) == c["carry"]
+    for ctx in set(ctxs):
+        assert ctx.last_device_error() == 0
+    del batches, results
+    torch.cuda.empty_cache()
+
+
+def test_device_error_word_reads_zero_after_clean_decodes(ws):
+    dec = ws.frame_decoder()
+    src = streams.case_bytes("random_frames_200")
+    view, _ = dev_bytes(src)
+    dec.decode(view, cap=8)
+    assert dec.ctx.last_device_error() == 0
+    assert dec.ctx.last_device_error() == 0

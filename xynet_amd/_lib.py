@@ -13,6 +13,14 @@ ROOT = os.path.dirname(PKG)
 HEADER = os.path.join(ROOT, "include", "xyws.h")
 
 XYWS_OK = 0
+XYWS_ERR_DEVICE = -5
+NSTATS = 48  # XYWS_NSTATS (xyws_stream.h)
+R_WORDS = 32  # u64 words per run record (xyws_stream.hip)
+# internal decode options (xyws_stream.h; not part of include/xyws.h)
+OPT_STATS = 0x100
+OPT_SMALL_SEG = 0x200
+OPT_WG512 = 0x40000
+OPT_TEST_GIVEUP = 0x100000
 ERRORS = {-1: "invalid argument", -2: "HIP runtime error", -3: "device allocation failed",
           -4: "scratch capacity exceeded", -5: "device-side error"}
 
@@ -84,9 +92,9 @@ def load():
     L.xyws_decode_indexed.restype = i32
     L.xyws_decode_indexed.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp]
     L.xyws_debug_stats.restype = i32
-    L.xyws_debug_stats.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.xyws_debug_stats.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
     L.xyws_debug_records.restype = C.c_int64
-    L.xyws_debug_records.argtypes = [vp, C.POINTER(C.c_uint64), u64]
+    L.xyws_debug_records.argtypes = [vp, vp, C.POINTER(C.c_uint64), u64]
     L.xyws_decode_stream.restype = i32
     L.xyws_decode_stream.argtypes = [vp, vp, u64, vp, vp, vp, u64, vp, u32, vp]
     _lib = L

@@ -274,15 +274,33 @@ __global__ void __launch_bounds__(UNMASK_THREADS) k_unmask_tiles(uint8_t* __rest
 // ===========================================================================
 // C-ABI
 // ===========================================================================
-struct xyws_ctx {
-  int device;
-  std::mutex mu;
+// Device scratch is kept per (context, stream): a decode's run records, flags
+// and frame table belong to the stream it was enqueued on, so calls on one
+// context from several streams (an io_uring service overlapping batches) run
+// concurrently without sharing scratch. XYWS_SLOTS streams get a slot each;
+// a further stream takes the least recently used slot after waiting (on the
+// device, hipStreamWaitEvent) for that slot's last call.
+#define XYWS_SLOTS 8
+
+struct scratch_slot {
+  bool bound;
+  hipStream_t stream;
+  uint64_t last_use;
+  hipEvent_t ev;      // recorded after the slot's last call (not while capturing)
+  bool ev_valid;
   // frame table scratch (indexed + serial modes)
   void* tab_mem;
   uint64_t tab_cap;
-  uint64_t* tab_count;
-  uint32_t* err;  // device error word
   stream_scratch ss;  // fused stream decoder scratch (xyws_stream.hip)
+};
+
+struct xyws_ctx {
+  int device;
+  std::mutex mu;
+  uint32_t* err;  // device error word (serial / indexed modes)
+  uint64_t clock;
+  uint64_t reserve_bytes, reserve_frames;  // applied to every slot
+  scratch_slot slot[XYWS_SLOTS];
 };
 
 namespace {
@@ -301,30 +319,35 @@ struct device_guard {
 
 int hip_err(hipError_t e) { return e == hipSuccess ? XYWS_OK : XYWS_ERR_HIP; }
 
-int ensure_table(xyws_ctx* ctx, uint64_t n) {
-  if (n <= ctx->tab_cap && ctx->tab_mem) return XYWS_OK;
+bool capturing(hipStream_t s) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  (void)cs;
+  (void)hipStreamIsCapturing(s, &cs);
+  return cs != hipStreamCaptureStatusNone;
+}
+
+int ensure_table(scratch_slot* sl, uint64_t n, bool capture) {
+  if (n <= sl->tab_cap && sl->tab_mem) return XYWS_OK;
+  if (capture) return XYWS_ERR_CAPACITY;
   uint64_t cap = n < 1024 ? 1024 : n;
   void* mem = nullptr;
   size_t bytes = cap * (8 + 8 + 8 + 4) + 64;
   if (hipMalloc(&mem, bytes) != hipSuccess) return XYWS_ERR_NOMEM;
-  if (ctx->tab_mem) {
+  if (sl->tab_mem) {
     (void)hipDeviceSynchronize();
-    (void)hipFree(ctx->tab_mem);
+    (void)hipFree(sl->tab_mem);
   }
-  ctx->tab_mem = mem;
-  ctx->tab_cap = cap;
+  sl->tab_mem = mem;
+  sl->tab_cap = cap;
   return XYWS_OK;
 }
 
-frame_table table_of(xyws_ctx* ctx) {
+frame_table table_of(scratch_slot* sl) {
   frame_table t;
-  char* m = static_cast<char*>(ctx->tab_mem);
+  char* m = static_cast<char*>(sl->tab_mem);
   t.start = reinterpret_cast<uint64_t*>(m);
-  t.ps = t.start + ctx->tab_cap;
-  t.pe = t.ps + ctx->tab_cap;
-  t.count = t.pe + ctx->tab_cap;
+  t.ps = t.start + sl->tab_cap;
+  t.pe = t.ps + sl->tab_cap;
+  t.count = t.pe + sl->tab_cap;
   t.kw = reinterpret_cast<uint32_t*>(t.count + 8);
   return t;
 }
@@ -334,6 +357,38 @@ int grid_for(uint64_t items, uint32_t per_block, uint32_t cap) {
   if (g < 1) g = 1;
   if (g > cap) g = cap;
   return (int)g;
+}
+
+// The slot of `stream` (ctx->mu held).
+int acquire_slot(xyws_ctx* ctx, hipStream_t stream, bool capture, scratch_slot** out) {
+  scratch_slot* pick = nullptr;
+  for (auto& sl : ctx->slot)
+    if (sl.bound && sl.stream == stream) { pick = &sl; break; }
+  if (!pick)
+    for (auto& sl : ctx->slot)
+      if (!sl.bound) { pick = &sl; break; }
+  if (!pick) {
+    for (auto& sl : ctx->slot)
+      if (!pick || sl.last_use < pick->last_use) pick = &sl;
+    if (pick->ev_valid) {
+      if (capture) return XYWS_ERR_CAPACITY;  // (an event from outside the capture)
+      if (hipStreamWaitEvent(stream, pick->ev, 0) != hipSuccess) return XYWS_ERR_HIP;
+    }
+  }
+  pick->bound = true;
+  pick->stream = stream;
+  pick->last_use = ++ctx->clock;
+  *out = pick;
+  return XYWS_OK;
+}
+
+// After enqueueing a call on the slot: its completion event.
+int release_slot(scratch_slot* sl, hipStream_t stream, bool capture) {
+  if (capture) return XYWS_OK;
+  if (!sl->ev && hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming) != hipSuccess) return XYWS_ERR_HIP;
+  if (hipEventRecord(sl->ev, stream) != hipSuccess) return XYWS_ERR_HIP;
+  sl->ev_valid = true;
+  return XYWS_OK;
 }
 
 }  // namespace
@@ -364,10 +419,20 @@ int xyws_ctx_create(int device, xyws_ctx** out) {
   if (!g.ok) return XYWS_ERR_HIP;
   xyws_ctx* c = new xyws_ctx();
   c->device = device;
-  c->tab_mem = nullptr;
-  c->tab_cap = 0;
   c->err = nullptr;
-  stream_scratch_init(&c->ss, device);
+  c->clock = 0;
+  c->reserve_bytes = 0;
+  c->reserve_frames = 0;
+  for (auto& sl : c->slot) {
+    sl.bound = false;
+    sl.stream = nullptr;
+    sl.last_use = 0;
+    sl.ev = nullptr;
+    sl.ev_valid = false;
+    sl.tab_mem = nullptr;
+    sl.tab_cap = 0;
+    stream_scratch_init(&sl.ss, device);
+  }
   if (hipMalloc(&c->err, 64) != hipSuccess) {
     delete c;
     return XYWS_ERR_NOMEM;
@@ -386,9 +451,12 @@ int xyws_ctx_destroy(xyws_ctx* ctx) {
   {
     device_guard g(ctx->device);
     (void)hipDeviceSynchronize();
-    if (ctx->tab_mem) (void)hipFree(ctx->tab_mem);
+    for (auto& sl : ctx->slot) {
+      if (sl.tab_mem) (void)hipFree(sl.tab_mem);
+      if (sl.ev) (void)hipEventDestroy(sl.ev);
+      stream_scratch_free(&sl.ss);
+    }
     if (ctx->err) (void)hipFree(ctx->err);
-    stream_scratch_free(&ctx->ss);
   }
   delete ctx;
   return XYWS_OK;
@@ -399,36 +467,54 @@ int xyws_ctx_reserve(xyws_ctx* ctx, uint64_t max_batch_bytes, uint64_t max_frame
   std::lock_guard<std::mutex> lk(ctx->mu);
   device_guard g(ctx->device);
   if (!g.ok) return XYWS_ERR_HIP;
-  int rc = ensure_table(ctx, max_frames);
-  if (rc) return rc;
-  return stream_scratch_reserve(&ctx->ss, max_batch_bytes);
+  if (max_batch_bytes > ctx->reserve_bytes) ctx->reserve_bytes = max_batch_bytes;
+  if (max_frames > ctx->reserve_frames) ctx->reserve_frames = max_frames;
+  for (auto& sl : ctx->slot) {
+    if (ctx->reserve_frames) {
+      int rc = ensure_table(&sl, ctx->reserve_frames, false);
+      if (rc) return rc;
+    }
+    int rc = stream_scratch_reserve(&sl.ss, ctx->reserve_bytes);
+    if (rc) return rc;
+  }
+  return XYWS_OK;
 }
 
 int xyws_ctx_last_device_error(xyws_ctx* ctx, uint32_t* out) {
   if (!ctx || !out) return XYWS_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
   device_guard g(ctx->device);
   if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
-  uint32_t v[2] = {0, 0};
-  if (hipMemcpy(v, ctx->err, 4, hipMemcpyDeviceToHost) != hipSuccess) return XYWS_ERR_HIP;
-  *out = v[0] | stream_scratch_error(&ctx->ss);
-  return XYWS_OK;
+  uint32_t v = 0;
+  if (hipMemcpy(&v, ctx->err, 4, hipMemcpyDeviceToHost) != hipSuccess) return XYWS_ERR_HIP;
+  if (v && hipMemset(ctx->err, 0, 4) != hipSuccess) return XYWS_ERR_HIP;
+  for (auto& sl : ctx->slot) v |= stream_scratch_error(&sl.ss, true);
+  *out = v;
+  return v ? XYWS_ERR_DEVICE : XYWS_OK;
 }
 
 // Internal (not part of include/xyws.h): resolution counters of the last fused
-// stream decode run with XYWS_OPT_STATS (0x100). Synchronizes the device.
-int xyws_debug_stats(xyws_ctx* ctx, uint64_t out[32]) {
+// stream decode run with XYWS_OPT_STATS (0x100) on `stream`. Synchronizes the
+// device. out: XYWS_NSTATS words.
+int xyws_debug_stats(xyws_ctx* ctx, void* stream, uint64_t* out) {
   if (!ctx || !out) return XYWS_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
   device_guard g(ctx->device);
-  return stream_scratch_stats(&ctx->ss, out);
+  for (auto& sl : ctx->slot)
+    if (sl.bound && sl.stream == (hipStream_t)stream) return stream_scratch_stats(&sl.ss, out);
+  return XYWS_ERR_INVALID;
 }
 
-// Internal: the run records of the last fused stream decode (24 u64 per run,
-// layout in xyws_stream.hip), at most max_runs of them; returns the count
-// copied or a negative error. Synchronizes the device.
-int64_t xyws_debug_records(xyws_ctx* ctx, uint64_t* out, uint64_t max_runs) {
+// Internal: the run records of the last fused stream decode on `stream`, at
+// most max_runs of them; returns the count copied or a negative error.
+// Synchronizes the device.
+int64_t xyws_debug_records(xyws_ctx* ctx, void* stream, uint64_t* out, uint64_t max_runs) {
   if (!ctx || !out) return XYWS_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
   device_guard g(ctx->device);
-  return stream_scratch_records(&ctx->ss, out, max_runs);
+  for (auto& sl : ctx->slot)
+    if (sl.bound && sl.stream == (hipStream_t)stream) return stream_scratch_records(&sl.ss, out, max_runs);
+  return XYWS_ERR_INVALID;
 }
 
 int xyws_unmask(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4], uint64_t phase,
@@ -459,13 +545,16 @@ int xyws_decode_indexed(xyws_ctx* ctx, void* dev_buf, uint64_t len, const uint64
   std::lock_guard<std::mutex> lk(ctx->mu);
   device_guard g(ctx->device);
   if (!g.ok) return XYWS_ERR_HIP;
-  int rc = ensure_table(ctx, n);
+  hipStream_t s = (hipStream_t)stream;
+  const bool cap = capturing(s);
+  scratch_slot* sl = nullptr;
+  int rc = acquire_slot(ctx, s, cap, &sl);
   if (rc) return rc;
+  if ((rc = ensure_table(sl, n, cap))) return rc;
   const uintptr_t addr = reinterpret_cast<uintptr_t>(dev_buf);
   uint8_t* base = reinterpret_cast<uint8_t*>(addr & ~(uintptr_t)15);
   const uint64_t lo = addr & 15, hi = lo + len;
-  frame_table t = table_of(ctx);
-  hipStream_t s = (hipStream_t)stream;
+  frame_table t = table_of(sl);
   hipLaunchKernelGGL(k_parse_indexed, dim3(grid_for(n, 256, 1u << 30)), dim3(256), 0, s, base, lo, hi,
                      dev_starts, n, t, dev_frames);
   if ((rc = hip_err(hipGetLastError()))) return rc;
@@ -473,9 +562,9 @@ int xyws_decode_indexed(xyws_ctx* ctx, void* dev_buf, uint64_t len, const uint64
     const uint64_t tiles = (hi - (lo & ~(uint64_t)(UNMASK_TILE - 1)) + UNMASK_TILE - 1) / UNMASK_TILE;
     hipLaunchKernelGGL(k_unmask_tiles, dim3(grid_for(tiles, 1, 4096)), dim3(UNMASK_THREADS), 0, s,
                        base, lo, hi, t);
-    rc = hip_err(hipGetLastError());
+    if ((rc = hip_err(hipGetLastError()))) return rc;
   }
-  return rc;
+  return release_slot(sl, s, cap);
 }
 
 int xyws_decode_stream(xyws_ctx* ctx, void* dev_buf, uint64_t len, const xyws_carry* dev_carry_in,
@@ -490,27 +579,32 @@ int xyws_decode_stream(xyws_ctx* ctx, void* dev_buf, uint64_t len, const xyws_ca
   uint8_t* base = reinterpret_cast<uint8_t*>(addr & ~(uintptr_t)15);
   const uint64_t lo = addr & 15, hi = lo + len;
   hipStream_t s = (hipStream_t)stream;
+  const bool capt = capturing(s);
+  scratch_slot* sl = nullptr;
+  int rc = acquire_slot(ctx, s, capt, &sl);
+  if (rc) return rc;
   if ((opts & XYWS_OPT_SERIAL_SCAN) || !XYWS_HAVE_FUSED) {
     // worst case is a 2-byte unmasked frame every 2 bytes; the debug path caps
     // its table at 2^24 frames and flags the device error word beyond that.
     uint64_t want = len / 2 + 2;
     if (want > (1ull << 24)) want = 1ull << 24;
-    int rc = ensure_table(ctx, want);
-    if (rc) return rc;
-    frame_table t = table_of(ctx);
+    if ((rc = ensure_table(sl, want, capt))) return rc;
+    frame_table t = table_of(sl);
     hipLaunchKernelGGL(k_stream_serial, dim3(1), dim3(64), 0, s, base, lo, hi, dev_carry_in,
-                       dev_carry_out, t, ctx->tab_cap, dev_frames, cap, dev_nframes, ctx->err);
+                       dev_carry_out, t, sl->tab_cap, dev_frames, cap, dev_nframes, ctx->err);
     if ((rc = hip_err(hipGetLastError()))) return rc;
     if (!(opts & XYWS_OPT_PARSE_ONLY) && len) {
       const uint64_t tiles = (hi - (lo & ~(uint64_t)(UNMASK_TILE - 1)) + UNMASK_TILE - 1) / UNMASK_TILE;
       hipLaunchKernelGGL(k_unmask_tiles, dim3(grid_for(tiles, 1, 4096)), dim3(UNMASK_THREADS), 0, s,
                          base, lo, hi, t);
-      rc = hip_err(hipGetLastError());
+      if ((rc = hip_err(hipGetLastError()))) return rc;
     }
-    return rc;
+    return release_slot(sl, s, capt);
   }
-  return stream_decode_fused(&ctx->ss, base, lo, hi, dev_carry_in, dev_carry_out, dev_frames, cap,
-                             dev_nframes, opts, s);
+  rc = stream_decode_fused(&sl->ss, base, lo, hi, dev_carry_in, dev_carry_out, dev_frames, cap,
+                           dev_nframes, opts, s);
+  if (rc) return rc;
+  return release_slot(sl, s, capt);
 }
 
 }  // extern "C"

@@ -18,6 +18,14 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // 16-byte-aligned address at or below the caller's buffer. The caller's bytes
 // are [lo, hi) in that coordinate system (lo = buf & 15).
 
+// A workgroup-uniform value read from LDS, moved to scalar registers (values
+// loaded from LDS live in VGPRs otherwise, where the store loops need them).
+XYWS_DEV uint32_t uniform32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+XYWS_DEV uint64_t uniform64(uint64_t v) {
+  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+}
+
 // Rotate a little-endian key word so byte t of the result XORs a byte whose
 // payload index is congruent to t + c (mod 4).
 XYWS_DEV uint32_t rotr8(uint32_t k, uint32_t c) {

@@ -16,8 +16,12 @@ struct stream_scratch {
 void stream_scratch_init(stream_scratch* s, int device);
 void stream_scratch_free(stream_scratch* s);
 int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes);
-uint32_t stream_scratch_error(stream_scratch* s);
-int stream_scratch_stats(stream_scratch* s, uint64_t out[32]);
+// sticky device error word of this scratch (bit 1: an inter-workgroup wait
+// timed out, bit 2: a run record was not written by its call); clear: reset
+// it after reading (the device must be idle)
+uint32_t stream_scratch_error(stream_scratch* s, bool clear);
+#define XYWS_NSTATS 48
+int stream_scratch_stats(stream_scratch* s, uint64_t out[XYWS_NSTATS]);
 int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_runs);
 
 // Internal decode options (not part of include/xyws.h):
@@ -27,6 +31,8 @@ int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_ru
 #define XYWS_OPT_NO_STORE 0x20000u // diagnostics: decode without writing (timing split only)
 #define XYWS_OPT_WG512 0x40000u    // two 512-thread workgroups per CU, 64 KiB segments
 #define XYWS_OPT_DIAG 0x80000u     // diagnostics: no prefetch during the prologue scan (timing only)
+#define XYWS_OPT_TEST_GIVEUP 0x100000u // tests: odd runs give up on their successor at once (the path
+                                       // of a successor whose workgroup has not started; finish bridges it)
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
                         const xyws_carry* cin, xyws_carry* cout, xyws_frame* frames, uint64_t cap,
                         uint64_t* nframes, uint32_t opts, hipStream_t stream);

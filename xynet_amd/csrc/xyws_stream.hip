@@ -52,12 +52,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "xyws_stream.h"
 #include "xyws_device.h"
 
 namespace {
 
 constexpr uint64_t NONE = ~0ull;
+constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr uint32_t PAD = 32;          // LDS bytes after the segment (5-dword header reads)
 // Headers a speculative entry's chain must pass, by the entry's length form:
 // a false 127-form header needs 0xFF/0x7F plus an 8-byte length below 2^46
@@ -114,14 +117,34 @@ struct cstate {
   uint32_t pad;
 };
 
+// k_stream_finish's walk: the current chain piece (see the walk below).
+struct walk_t {
+  cstate F;
+  uint64_t r, efrom, cnt, tail, first, succ, wlim;
+  uint32_t ok, tmo, ecarry, act;
+};
+
 // run record: R_WORDS x u64
 enum {
   R_H = 0, R_W, R_S0, R_HEAD = R_S0 + 5,            // prologue: entry, write start, state, head frames
-  R_OK = 8, R_HN, R_WN, R_CNT, R_TAIL, R_FIRST,     // results (R_OK: ok | succ << 32)
+  R_OK = 8, R_HN, R_WN, R_CNT, R_TAIL, R_FIRST,     // results (R_OK: ok | tmo << 1 | succ << 32)
   R_F0 = 14,                                        // final state (5 words)
   R_EFROM = 20, R_ECNT, R_EORD, R_ECARRY,           // emission plan (k_stream_finish)
-  R_WORDS = 24
+  R_EP = 24,                                        // epoch of the call that wrote the results
+  R_WORDS = 32
 };
+// R_OK bits
+constexpr uint64_t OK_BIT = 1, TMO_BIT = 2;  // chain landed on the successor; successor wait timed out
+
+// Prologue flags, one u64 per run, stamped with the call's epoch E (head word
+// HEAD_EPOCH holds the number of completed calls; a call runs with E = that +
+// 1): (E << 1) = claimed in this call (by the run's own workgroup),
+// (E << 1) | 1 = published. Anything below E << 1 is a previous call's and
+// reads as unclaimed, so no per-call reset is needed and a stale record is
+// never taken for a live one.
+XYWS_DEV uint64_t flag_claimed(uint64_t E) { return E << 1; }
+XYWS_DEV uint64_t flag_published(uint64_t E) { return (E << 1) | 1u; }
+constexpr uint32_t HEAD_EPOCH = 4;  // u32 index of the u64 epoch word in head[]
 
 struct run_params {
   uint8_t* base;
@@ -135,8 +158,8 @@ struct run_params {
   uint64_t cap;
   uint64_t* nframes;
   uint64_t* rec;          // R_WORDS per run
-  uint32_t* flags;        // per run: 1 = prologue published
-  uint32_t* head;         // [0] ticket, [1] error word, [2..3] u64 total; stats at [32..)
+  uint64_t* flags;        // per run: prologue claim/publish word (epoch-stamped, see flag_claimed)
+  uint32_t* head;         // [0] ticket, [1] error word, [2..3] u64 total, [4..5] u64 epoch; stats at [32..)
   uint32_t opts;
 };
 
@@ -153,7 +176,11 @@ struct __attribute__((aligned(16))) lds_t {
   cstate S;
   cstate B;  // k_stream_finish: exact state handed to a repaired run
   uint64_t hn, Wn, succ, first_after, cnt, tail, aux0, aux1, aux2, bcnt, bfirst;
+  uint64_t E;      // this call's epoch
+  uint64_t scan_j; // successor lookup: next run to examine
+  walk_t wk;       // k_stream_finish: the current chain piece
   uint32_t nfl, pass_hi, known, past, ok, done, end, best, ticket, act, repaired, ccnt, ucnt, keepn, ovf;
+  uint32_t tmo;    // successor given up on (write limit = own range end, bridged by k_stream_finish)
   // per 1 KiB row of the segment (one wave-instruction of chunks), set by
   // wave 0 after each chase pass: ROW_FAST (one key word for the whole row,
   // rk), ROW_SKIP (nothing to store) or the entry to start the walk from
@@ -172,14 +199,13 @@ XYWS_DEV void st_store(uint64_t* p, uint64_t v) {
 XYWS_DEV uint64_t st_load(const uint64_t* p) {
   return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-XYWS_DEV uint32_t flag_load(const uint32_t* p) {
-  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+XYWS_DEV uint64_t flag_load(const uint64_t* p) { return st_load(p); }
 XYWS_DEV bool stats_on(const run_params& P) { return (P.opts & XYWS_OPT_STATS) != 0; }
 enum { ST_RUNS = 0, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRAMES,
        ST_P_WIN, ST_P_CAND, ST_P_UND, ST_P_TCOMP, ST_P_TCHECK, ST_P_TRES, ST_D_TENT, ST_D_TCHASE,
        ST_T_PRO = 16, ST_T_MAIN, ST_T_WAIT, ST_T_FILL, ST_T_CHASE, ST_T_XOR, ST_T_TAIL, ST_T_PF, ST_T_CP,
-       ST_P_FILL, ST_P_SCAN, ST_P_PUB, ST_D_NOENT, ST_D_CHASE, ST_D_MISMATCH, ST_D_OVF };
+       ST_P_FILL, ST_P_SCAN, ST_P_PUB, ST_D_NOENT, ST_D_CHASE, ST_D_MISMATCH, ST_D_OVF,
+       ST_GIVEUP = 32, ST_BRIDGE };
 XYWS_DEV void stat_add(const run_params& P, uint32_t i, uint64_t v) {
   if (stats_on(P)) atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + i, (unsigned long long)v);
 }
@@ -574,7 +600,7 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
 // continues it. Called only where no limit lies in the segment.
 template <class G>
 XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid, bool unm, bool past) {
-  constexpr uint32_t NSB = G::NSB, SB = G::SB, SECT = G::SECT, NONE32 = 0xFFFFFFFFu;
+  constexpr uint32_t NSB = G::NSB, SB = G::SB, SECT = G::SECT;
   constexpr uint32_t STOP = G::SEG - XYWS_MAX_FRAME_HEADER_SIZE + 1;  // headers wholly in LDS start below
   const uint32_t lane = tid & 63u, gl = lane & 15u, sb = (tid >> 6) * 4 + (lane >> 4);
   const cstate S0 = L.S;
@@ -800,29 +826,69 @@ XYWS_DEV void build_rows(lds_t<G>& L, uint32_t nfl, uint32_t lo_c, uint32_t hi_c
   }
 }
 
-// The next run after `run` that has an entry (lane 0). Waits for each
-// candidate's prologue; every one of them took its ticket after ours.
-XYWS_DEV void lookup_successor(const run_params& P, uint64_t& hn, uint64_t& Wn, uint64_t& succ, uint32_t run) {
-  for (uint32_t j = run + 1; j < P.nruns; j++) {
-    uint32_t it = 0;
-    while (flag_load(P.flags + j) == 0u && it < SPIN) {
-      __builtin_amdgcn_s_sleep(2);
-      it++;
+// Wait until run j's prologue, claimed in this call, is published (lane 0).
+// The claimer is run j's own running workgroup, which computes the prologue
+// without waiting for anything, so the wait ends; the bound only reports a bug.
+XYWS_DEV bool wait_published(const run_params& P, uint32_t j, uint64_t E) {
+  const uint64_t want = flag_published(E);
+  uint32_t it = 0;
+  while (flag_load(P.flags + j) != want && it < SPIN) {
+    __builtin_amdgcn_s_sleep(2);
+    it++;
+  }
+  if (it) stat_add(P, ST_SPIN, it);
+  if (it >= SPIN) {
+    atomicOr(P.head + 1, 2u);
+    return false;
+  }
+  return true;
+}
+
+// The next run after `run` that has an entry (lane 0), starting the search at
+// L.scan_j. Returns LK_FOUND with (hn, Wn, succ) (succ = nruns: none), or
+// LK_GIVEUP with succ = the run whose prologue is not published: its workgroup
+// has not started (not every workgroup of the grid is resident, e.g. beside a
+// concurrent decode, and waiting for one that is not could deadlock), or its
+// bounded wait timed out (reported in the error word). Never reads a record
+// whose flag is not published in this call. A run given up on is bridged by
+// k_stream_finish.
+enum { LK_FOUND = 0, LK_GIVEUP = 1 };
+template <class G>
+XYWS_DEV uint32_t lookup_successor(const run_params& P, lds_t<G>& L, uint64_t& hn, uint64_t& Wn, uint64_t& succ,
+                                   uint32_t run) {
+  const uint64_t E = L.E;
+  for (uint64_t j = L.scan_j; j < P.nruns; j++) {
+    L.scan_j = j;
+    // (test mode: odd runs give up on their successor at once)
+    const bool test = (P.opts & XYWS_OPT_TEST_GIVEUP) && (run & 1u);
+    if (test || (flag_load(P.flags + j) >> 1) < E || !wait_published(P, (uint32_t)j, E)) {
+      succ = j;
+      return LK_GIVEUP;
     }
-    if (it) stat_add(P, ST_SPIN, it);
-    if (it >= SPIN) atomicOr(P.head + 1, 2u);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint64_t h = st_load(P.rec + (uint64_t)j * R_WORDS + R_H);
+    const uint64_t h = st_load(P.rec + j * R_WORDS + R_H);
     if (h != NONE) {
       hn = h;
-      Wn = st_load(P.rec + (uint64_t)j * R_WORDS + R_W);
+      Wn = st_load(P.rec + j * R_WORDS + R_W);
       succ = j;
-      return;
+      return LK_FOUND;
     }
   }
   hn = NONE;
   Wn = NONE;
   succ = P.nruns;
+  return LK_FOUND;
+}
+
+// CH dropped stores (out-of-range offset: no memory traffic) after loads into
+// `io`, so that on every path into the chain loop at least CH stores are
+// younger than the loads: the compiler's wait before the fill is then
+// vmcnt(CH), not vmcnt(0)
+template <class G>
+XYWS_DEV void dummy_stores(const run_params& P, uint64_t ss) {
+  const __amdgpu_buffer_rsrc_t rz = seg_rsrc<G>(P, ss);
+#pragma unroll
+  for (uint32_t k = 0; k < G::CH; k++)
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rz, OOB, k * G::NT * 16u, AUX_NT);  // distinct: not merged
 }
 
 // Apply the chain in L.S (set by lane 0 together with L.known/hn/Wn/succ and
@@ -841,15 +907,7 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
   // offset), so each fill waits for its loads only (vmcnt counts loads and
   // stores together, in issue order) while the previous segment's stores drain.
   if (!in_lds && io.pf != ss0) io.issue(P, ss0, tid, L.known ? L.Wn : NONE);
-  {
-    // CH dropped stores (out-of-range offset: no memory traffic) so that on
-    // every path into the loop at least CH stores are younger than the loads:
-    // the compiler's wait before the fill is then vmcnt(CH), not vmcnt(0)
-    const __amdgpu_buffer_rsrc_t rz = seg_rsrc<G>(P, ss0);
-#pragma unroll
-    for (uint32_t k = 0; k < G::CH; k++)
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rz, OOB, k * G::NT * 16u, AUX_NT);  // distinct: not merged
-  }
+  dummy_stores<G>(P, ss0);
   // stats builds: wave 0 accumulates phase cycles in registers, flushed once
   const bool st_on = stats_on(P) && tid < 64;
   uint64_t tm = st_on ? __builtin_amdgcn_s_memtime() : 0;
@@ -863,14 +921,19 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
     }                                                   \
   } while (0)
   // Once the next segment lies past the run's range the write limit is the
-  // successor's W (its prologue published it long ago): looked up one
-  // iteration ahead, so that every prefetch decision is known before the fill.
+  // successor's W (its prologue published it long ago): looked up before the
+  // next segment's prefetch is decided.
   auto lookup = [&](uint64_t nxt) {
     if (tid == 0 && !L.known && nxt >= rng_end) {
       const uint64_t t0 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
-      uint64_t hn, Wn, succ;
-      lookup_successor(P, hn, Wn, succ, run);
-      L.hn = hn; L.Wn = Wn; L.succ = succ; L.known = 1;
+      uint64_t hn = NONE, Wn = NONE, succ = P.nruns;
+      if (lookup_successor(P, L, hn, Wn, succ, run) == LK_GIVEUP) {
+        // unknown successor: write up to the own range end only and leave
+        // the rest to k_stream_finish (never a stale record)
+        L.hn = NONE; L.Wn = rng_end; L.succ = succ; L.known = 1; L.tmo = 1;
+      } else {
+        L.hn = hn; L.Wn = Wn; L.succ = succ; L.known = 1;
+      }
       if (stats_on(P)) stat_add(P, ST_T_WAIT, __builtin_amdgcn_s_memtime() - t0);
     }
   };
@@ -1307,21 +1370,77 @@ XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32
   __syncthreads();
 }
 
+// Prologue of run `run` (whole workgroup): the entry scan of its range, then
+// lane 0 publishes (h, W, entry state, head frames) in its record and sets its
+// flag to published for this call. The chain state is left in L, the scanned
+// segment in LDS (L.aux1), L.aux2 = W or NONE.
+template <class G>
+XYWS_DEV void prologue(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint32_t run) {
+  const uint64_t t0 = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
+  find_entry(P, L, io, tid, run);
+  const uint64_t tpub = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
+  if (tid == 0) {
+    const uint64_t rng_end = run + 1 < P.nruns ? (uint64_t)(run + 1) * P.rbytes : NONE;
+    const uint64_t q = L.aux0, ss = L.aux1;
+    uint64_t h = NONE, W = NONE, hc = 0;
+    cstate S;
+    S.X = 0; S.cov_ps = 0; S.cov_start = 0; S.cov_kw = 0; S.cov_key = 0; S.st = S_NOCOV; S.pad = 0;
+    if (q != NONE) {
+      const hdr_info hq = hdr_at(P, L, ss, q, NONE);
+      h = (hq.hlen == 2 || hq.hlen == 6) ? sat_add(q + hq.hlen, hq.plen) : q;
+      const hdr_info hh = h < P.hi ? hdr_at(P, L, ss, h, NONE) : hq;
+      if (h >= rng_end || h >= P.hi || !hh.hlen) {
+        h = NONE;
+      } else {
+        W = (h + hh.hlen + 15) & ~15ull;
+        // frames starting below W: parsed here, from bytes nobody writes yet
+        S = frame_state(h, hh);
+        hc = 1;
+        while (S.X < W && S.X < P.hi) {
+          const hdr_info hx = hdr_at(P, L, ss, S.X, NONE);
+          if (!hx.hlen) { S.st |= S_PARTIAL; break; }
+          S = frame_state(S.X, hx);
+          hc++;
+        }
+      }
+    }
+    uint64_t* rec = P.rec + (uint64_t)run * R_WORDS;
+    st_store(rec + R_H, h);
+    st_store(rec + R_W, W);
+    put_state(rec + R_S0, S);
+    st_store(rec + R_HEAD, hc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(P.flags + run, flag_published(L.E), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    L.S = S;
+    L.cnt = hc;
+    // dense-pass hint for the first segment: the entry's frame is small
+    L.dense = (h != NONE && S.X - S.cov_start < 1024) ? G::FCAP : 0;
+    L.aux2 = h == NONE ? NONE : W;
+    stat_add(P, ST_RUNS, 1);
+    if (h == NONE) stat_add(P, ST_NONE, 1);
+    if (stats_on(P)) stat_add(P, ST_T_PRO, __builtin_amdgcn_s_memtime() - t0);
+    if (stats_on(P)) stat_add(P, ST_P_PUB, __builtin_amdgcn_s_memtime() - tpub);
+  }
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------- kernels
 template <class G>
 __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
   lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
   const uint32_t tid = threadIdx.x;
-  if (tid == 0) L.ticket = atomicAdd(P.head, 1u);
+  if (tid == 0) {
+    L.ticket = atomicAdd(P.head, 1u);
+    L.E = st_load(reinterpret_cast<const uint64_t*>(P.head + HEAD_EPOCH)) + 1;
+  }
   __syncthreads();
-  const uint32_t run = L.ticket;
+  const uint32_t run = uniform32(L.ticket);
   if (run >= P.nruns) return;
   uint64_t* rec = P.rec + (uint64_t)run * R_WORDS;
   if (tid == 0) st_store(rec + R_ECNT, 0);  // no descriptors unless k_stream_finish plans them
   const uint64_t rng_end = run + 1 < P.nruns ? (uint64_t)(run + 1) * P.rbytes : NONE;
   seg_io<G> io;
-  uint64_t t0 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
   uint64_t wlo, ss0;
   bool in_lds = false;
   if (run == 0) {
@@ -1346,79 +1465,84 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
     wlo = P.lo;
     ss0 = 0;
   } else {
-    find_entry(P, L, io, tid, run);
-    const uint64_t tpub = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
-    if (tid == 0) {
-      const uint64_t q = L.aux0, ss = L.aux1;
-      uint64_t h = NONE, W = NONE, hc = 0;
-      cstate S;
-      S.X = 0; S.cov_ps = 0; S.cov_start = 0; S.cov_kw = 0; S.cov_key = 0; S.st = S_NOCOV; S.pad = 0;
-      if (q != NONE) {
-        const hdr_info hq = hdr_at(P, L, ss, q, NONE);
-        h = (hq.hlen == 2 || hq.hlen == 6) ? sat_add(q + hq.hlen, hq.plen) : q;
-        const hdr_info hh = h < P.hi ? hdr_at(P, L, ss, h, NONE) : hq;
-        if (h >= rng_end || h >= P.hi || !hh.hlen) {
-          h = NONE;
-        } else {
-          W = (h + hh.hlen + 15) & ~15ull;
-          // frames starting below W: parsed here, from bytes nobody writes yet
-          S = frame_state(h, hh);
-          hc = 1;
-          while (S.X < W && S.X < P.hi) {
-            const hdr_info hx = hdr_at(P, L, ss, S.X, NONE);
-            if (!hx.hlen) { S.st |= S_PARTIAL; break; }
-            S = frame_state(S.X, hx);
-            hc++;
-          }
-        }
-      }
-      st_store(rec + R_H, h);
-      st_store(rec + R_W, W);
-      put_state(rec + R_S0, S);
-      st_store(rec + R_HEAD, hc);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(P.flags + run, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      L.S = S;
-      L.cnt = hc;
-      // dense-pass hint for the first segment: the entry's frame is small
-      L.dense = (h != NONE && S.X - S.cov_start < 1024) ? G::FCAP : 0;
-      L.aux2 = h == NONE ? NONE : W;
-      stat_add(P, ST_RUNS, 1);
-      if (h == NONE) stat_add(P, ST_NONE, 1);
-      if (stats_on(P)) stat_add(P, ST_T_PRO, __builtin_amdgcn_s_memtime() - t0);
-      if (stats_on(P)) stat_add(P, ST_P_PUB, __builtin_amdgcn_s_memtime() - tpub);
-    }
-    __syncthreads();
+    // claim the own prologue (a predecessor that finds it unclaimed gives up
+    // on this run instead of waiting for a workgroup that may not be running)
+    if (tid == 0)
+      __hip_atomic_store(P.flags + run, flag_claimed(L.E), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prologue<G>(P, L, io, tid, run);
     if (L.aux2 == NONE) return;  // no entry: the chain of an earlier run covers this range
-    wlo = L.aux2;
+    wlo = uniform64(L.aux2);
     // the chain starts in the scanned segment (usual) or on the grid after it
-    ss0 = L.aux1 + (wlo - L.aux1) / G::SEG * G::SEG;
-    in_lds = ss0 == L.aux1;
+    const uint64_t a1 = uniform64(L.aux1);
+    ss0 = a1 + (wlo - a1) / G::SEG * G::SEG;
+    in_lds = ss0 == a1;
     // (the next segment's loads were issued before the scan)
     if (in_lds && ss0 + G::SEG < P.hi && io.pf != ss0 + G::SEG) io.issue(P, ss0 + G::SEG, tid);
   }
   if (tid == 0) {
-    L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.first_after = NONE;
+    L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.tmo = 0; L.first_after = NONE;
     if (run == 0) L.dense = 0;
     L.known = rng_end == NONE;
-    L.hn = NONE; L.Wn = NONE; L.succ = P.nruns;
+    L.hn = NONE; L.Wn = NONE; L.succ = P.nruns; L.scan_j = run + 1;
   }
   __syncthreads();
   uint64_t t1 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
   run_chain(P, L, io, tid, ss0, in_lds, wlo, rng_end, run);
   if (tid == 0) {
-    const bool ok = L.succ >= P.nruns || (L.past && L.ok);
-    st_store(rec + R_OK, (uint64_t)(ok ? 1u : 0u) | ((uint64_t)L.succ << 32));
+    uint64_t* rec = P.rec + (uint64_t)run * R_WORDS;
+    const bool ok = !L.tmo && (L.succ >= P.nruns || (L.past && L.ok));
+    st_store(rec + R_OK, (ok ? OK_BIT : 0) | (L.tmo ? TMO_BIT : 0) | ((uint64_t)L.succ << 32));
     st_store(rec + R_HN, L.hn);
     st_store(rec + R_WN, L.Wn);
     st_store(rec + R_CNT, L.cnt);
     st_store(rec + R_TAIL, L.tail);
     st_store(rec + R_FIRST, L.first_after);
     put_state(rec + R_F0, L.S);
+    st_store(rec + R_EP, L.E);
     if (!ok) stat_add(P, ST_BAD, 1);
+    if (L.tmo) stat_add(P, ST_GIVEUP, 1);
     stat_add(P, ST_FRAMES, L.cnt);
     if (stats_on(P)) stat_add(P, ST_T_MAIN, __builtin_amdgcn_s_memtime() - t1);
   }
+}
+
+// The next run after r with an entry (lane 0; every prologue is published by
+// now), or nruns.
+XYWS_DEV uint64_t next_visible(const run_params& P, uint64_t r) {
+  for (uint64_t j = r + 1; j < P.nruns; j++)
+    if (st_load(P.rec + j * R_WORDS + R_H) != NONE) return j;
+  return P.nruns;
+}
+
+// The piece of run r as its workgroup recorded it (lane 0). Its hand-over is
+// good only if its record is this call's and its successor's published entry
+// is the one its chain landed on.
+XYWS_DEV void load_piece(const run_params& P, walk_t& w, uint64_t r) {
+  const uint64_t* rec = P.rec + r * R_WORDS;
+  const uint64_t okw = st_load(rec + R_OK);
+  w.r = r;
+  w.efrom = st_load(rec + R_H);
+  w.ecarry = r == 0 ? 1u : 0u;
+  w.cnt = st_load(rec + R_CNT);
+  w.tail = st_load(rec + R_TAIL);
+  w.first = st_load(rec + R_FIRST);
+  w.F = get_state(rec + R_F0);
+  w.wlim = st_load(rec + R_WN);
+  w.succ = okw >> 32;
+  w.tmo = (okw & TMO_BIT) ? 1u : 0u;
+  w.ok = (okw & OK_BIT) ? 1u : 0u;
+  if (w.ok && w.succ < P.nruns && st_load(rec + R_HN) != st_load(P.rec + w.succ * R_WORDS + R_H)) w.ok = 0;
+}
+
+// Set up a chase from state S with the given successor limits (lane 0).
+template <class G>
+XYWS_DEV void chain_start(lds_t<G>& L, const cstate& S, uint64_t hn, uint64_t Wn, uint64_t succ) {
+  L.S = S;
+  L.S.st &= ~S_CUT;
+  L.hn = hn; L.Wn = Wn; L.succ = succ;
+  L.known = 1; L.cnt = 0; L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.dense = 0; L.tmo = 0;
+  L.first_after = NONE;
+  L.best = 0;
 }
 
 // Walk the runs from run 0 along their successors, repairing every boundary
@@ -1430,18 +1554,25 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
   lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
   const uint32_t tid = threadIdx.x;
   seg_io<G> io;
-  // lane-0 walk state: aux0 = current run, aux2 = ordinal base; B/bcnt/bfirst:
-  // the exact state handed to a repaired run, the frames its predecessor chased
-  // into it and its first node; repaired: the current run's results are the
-  // redo's (left in L by run_chain)
+  const uint64_t E = st_load(reinterpret_cast<const uint64_t*>(P.head + HEAD_EPOCH)) + 1;
   // Fast path (every run with an entry landed exactly on its successor's
   // entry: the usual case): frame counts, descriptor ordinals and the final
-  // state by a block-wide scan over the run records, no serial walk.
+  // state by a block-wide scan over the run records, no serial walk. A run is
+  // good when its record is this call's, its successor wait did not time out,
+  // its chain landed on the successor's entry and that entry is the one the
+  // successor published.
   {
     uint64_t* scr = reinterpret_cast<uint64_t*>(L.seg);  // scratch: wave totals
+    // every run's entry, for the successor check (in LDS when it fits)
+    constexpr bool HS_LDS = G::SEG >= 1024 + 8 * MAX_RUNS;
+    uint64_t* hs = reinterpret_cast<uint64_t*>(L.seg + 1024);
+    if constexpr (HS_LDS) {
+      for (uint32_t r = tid; r < P.nruns; r += G::NT) hs[r] = st_load(P.rec + (uint64_t)r * R_WORDS + R_H);
+      __syncthreads();
+    }
     const uint32_t lane = tid & 63u, wave = tid >> 6;
     uint64_t carry = 0;
-    uint32_t bad = 0, last = 0;
+    uint32_t bad = 0, stale = 0, last = 0;
     bool has = false;
     cstate fsl;  // final state of this thread's last visible run
     for (uint32_t t0 = 0; t0 < P.nruns; t0 += G::NT) {
@@ -1450,19 +1581,27 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
       // every word this pass needs is loaded at once (one memory round trip
       // instead of three dependent ones; the final state of the last visible
       // run comes from its own thread)
-      uint64_t h = NONE, cw = 0, okw = 1;
+      uint64_t h = NONE, cw = 0, okw = OK_BIT, ep = E, hn = NONE;
       cstate fs;
       if (r < P.nruns) {
-        h = st_load(rec + R_H);
+        h = HS_LDS ? hs[r] : st_load(rec + R_H);
         cw = st_load(rec + R_CNT);
         okw = st_load(rec + R_OK);
+        ep = st_load(rec + R_EP);
+        hn = st_load(rec + R_HN);
         fs = get_state(rec + R_F0);
       }
       const bool vis = r < P.nruns && (r == 0 || h != NONE);
       const uint64_t cnt = vis ? cw : 0;
-      if (vis && !(okw & 1u)) bad = 1;
-      if (vis) last = r;
-      if (vis) { fsl = fs; has = true; }
+      if (vis) {
+        const uint64_t succ = okw >> 32;
+        if (ep != E) stale = 1;
+        if (!(okw & OK_BIT) || (okw & TMO_BIT) || ep != E) bad = 1;
+        if (succ < P.nruns && hn != (HS_LDS ? hs[succ] : st_load(P.rec + succ * R_WORDS + R_H))) bad = 1;
+        last = r;
+        fsl = fs;
+        has = true;
+      }
       uint64_t x = cnt;  // wave inclusive scan
 #pragma unroll
       for (uint32_t o = 1; o < 64; o <<= 1) {
@@ -1487,6 +1626,9 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
       carry += tot;
       __syncthreads();
     }
+    // a record not written by this call: a run did not complete (reported;
+    // the outputs of this call are invalid)
+    if (__syncthreads_or(stale) && tid == 0) atomicOr(P.head + 1, 4u);
     const bool any_bad = __syncthreads_or(bad);
     if (tid == 0) L.aux1 = 0;
     __syncthreads();
@@ -1497,100 +1639,124 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
       if (has && last == L.aux1) L.S = fsl;
       __syncthreads();
     }
-    if (any_bad) stat_add(P, ST_BAD, 0);
     if (tid == 0) L.act = any_bad ? 1u : 0u;
     __syncthreads();
   }
   if (L.act) {
-  if (tid == 0) { L.aux0 = 0; L.aux2 = 0; L.repaired = 0; }
+  // Serial walk with repairs. Lane 0 keeps the current chain piece in L.wk:
+  // the run whose descriptor plan it fills (r, efrom, ecarry), its frames
+  // (cnt; tail = those past the successor's entry), its final state F, its
+  // write limit, and how it hands over (ok / tmo / succ).
+  //  * tmo (the run gave up on a successor that had not started): bridge from
+  //    F, writing from the write limit, up to the next run with an entry; the
+  //    bridge's frames join the piece.
+  //  * !ok (the chain missed the successor's entry): undo the successor's run
+  //    (replaying its own chain: XOR is an involution and a chain never writes
+  //    its own header bytes), redo it from F, writing from the write limit; the
+  //    redo is the next piece.
+  //  * ok: the successor's own record is the next piece.
+  if (tid == 0) {
+    L.aux2 = 0;
+    load_piece(P, L.wk, 0);
+  }
   __syncthreads();
-  for (uint32_t guard = 0; guard <= 2 * P.nruns + 2; guard++) {
+  for (uint32_t guard = 0; guard <= 4 * P.nruns + 4; guard++) {
     if (tid == 0) {
-      const uint32_t r = (uint32_t)L.aux0;
-      uint64_t* rec = P.rec + (uint64_t)r * R_WORDS;
-      uint64_t ok, succ, cnt, tail, first, efrom;
-      cstate F;
-      if (L.repaired) {  // results of the redo (left in L by run_chain)
-        ok = L.succ >= P.nruns || (L.past && L.ok);
-        succ = L.succ;
-        cnt = L.bcnt + L.cnt;
-        tail = L.tail;
-        first = L.first_after;
-        F = L.S;
-        efrom = L.bfirst;
+      walk_t& w = L.wk;
+      if (w.tmo) {
+        const uint64_t sj = next_visible(P, w.r);
+        w.succ = sj;
+        w.act = 4;
+        stat_add(P, ST_BRIDGE, 1);
+        chain_start(L, w.F, sj < P.nruns ? st_load(P.rec + sj * R_WORDS + R_H) : NONE,
+                    sj < P.nruns ? st_load(P.rec + sj * R_WORDS + R_W) : NONE, sj);
       } else {
-        const uint64_t w = st_load(rec + R_OK);
-        ok = w & 1u;
-        succ = w >> 32;
-        cnt = st_load(rec + R_CNT);
-        tail = st_load(rec + R_TAIL);
-        first = st_load(rec + R_FIRST);
-        F = get_state(rec + R_F0);
-        efrom = st_load(rec + R_H);
-      }
-      st_store(rec + R_EFROM, efrom);
-      st_store(rec + R_ECNT, cnt);
-      st_store(rec + R_EORD, L.aux2);
-      st_store(rec + R_ECARRY, L.repaired ? 0u : (r == 0 ? 1u : 0u));
-      L.aux2 += cnt;
-      if (succ >= P.nruns) {
-        L.act = 0;  // done
-        L.S = F;
-      } else if (ok) {
-        L.act = 1;  // next run as recorded
-        L.aux0 = succ;
-        L.repaired = 0;
-      } else {
-        // boundary `succ` mis-speculated: undo its run, redo from our exact chain
-        stat_add(P, ST_REPAIR, 1);
-        const uint64_t* rs = P.rec + succ * R_WORDS;
-        L.B = F;
-        L.bcnt = tail;
-        L.bfirst = first != NONE ? first : F.X;
-        L.act = 2;
-        L.aux0 = succ;
-        L.S = get_state(rs + R_S0);
-        L.S.st &= ~S_CUT;
-        L.hn = st_load(rs + R_HN);
-        L.Wn = st_load(rs + R_WN);
-        L.succ = st_load(rs + R_OK) >> 32;
-        L.known = 1; L.cnt = 0; L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.dense = 0;
-        L.first_after = NONE;
-        L.best = 0;
+        uint64_t* rec = P.rec + w.r * R_WORDS;
+        st_store(rec + R_EFROM, w.efrom);
+        st_store(rec + R_ECNT, w.cnt);
+        st_store(rec + R_EORD, L.aux2);
+        st_store(rec + R_ECARRY, w.ecarry);
+        L.aux2 += w.cnt;
+        if (w.succ >= P.nruns) {
+          w.act = 0;  // done
+          L.S = w.F;
+        } else if (w.ok) {
+          w.act = 1;  // next run as recorded
+          load_piece(P, w, w.succ);
+        } else {
+          stat_add(P, ST_REPAIR, 1);
+          w.act = 2;
+          const uint64_t* rs = P.rec + w.succ * R_WORDS;
+          chain_start(L, get_state(rs + R_S0), st_load(rs + R_HN), st_load(rs + R_WN), st_load(rs + R_OK) >> 32);
+        }
       }
     }
     __syncthreads();
-    if (L.act == 0) break;
-    if (L.act == 1) continue;
-    // undo: replay the mis-speculated run exactly as it ran
-    const uint64_t* rs = P.rec + L.aux0 * R_WORDS;
+    const uint32_t act = L.wk.act;
+    if (act == 0) break;
+    if (act == 1) continue;
+    if (act == 4) {
+      // bridge: the chain from where the run stopped to the next entry
+      const uint64_t wp = L.wk.wlim;
+      io.pf = NONE;
+      run_chain(P, L, io, tid, wp & ~15ull, false, wp, NONE, 0);
+      __threadfence();
+      __syncthreads();
+      if (tid == 0) {
+        walk_t& w = L.wk;
+        w.cnt += L.cnt;
+        w.tail = L.tail;
+        w.first = L.first_after;
+        w.F = L.S;
+        w.ok = w.succ >= P.nruns || (L.past && L.ok);
+        w.wlim = L.Wn;
+        w.tmo = 0;
+      }
+      __syncthreads();
+      continue;
+    }
+    // act == 2: undo the successor's run exactly as it ran
+    const uint64_t sj = L.wk.succ;
+    const uint64_t* rs = P.rec + sj * R_WORDS;
     const uint64_t W = st_load(rs + R_W);
     const uint64_t hn = L.hn, Wn = L.Wn, succ = L.succ;
     io.pf = NONE;
     run_chain(P, L, io, tid, W & ~15ull, false, W, NONE, 0);
     __threadfence();  // the undo's stores are visible to the redo's loads
     __syncthreads();
-    // redo from the exact state, same successor
+    // redo from the exact state, same successor, from our write limit
+    const uint64_t wp = L.wk.wlim;
     if (tid == 0) {
-      L.S = L.B;
-      L.S.st &= ~S_CUT;
-      L.hn = hn; L.Wn = Wn; L.succ = succ;
-      L.known = 1; L.cnt = 0; L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.dense = 0;
-      L.first_after = NONE;
-      L.repaired = 1;
+      chain_start(L, L.wk.F, hn, Wn, succ);
     }
     __syncthreads();
     io.pf = NONE;
-    run_chain(P, L, io, tid, W & ~15ull, false, W, NONE, 0);
+    run_chain(P, L, io, tid, wp & ~15ull, false, wp, NONE, 0);
     __threadfence();
+    __syncthreads();
+    if (tid == 0) {
+      walk_t& w = L.wk;
+      const uint64_t ws = st_load(rs + R_OK);
+      w.efrom = w.first != NONE ? w.first : w.F.X;
+      w.cnt = w.tail + L.cnt;
+      w.r = sj;
+      w.ecarry = 0;
+      w.tail = L.tail;
+      w.first = L.first_after;
+      w.F = L.S;
+      w.succ = L.succ;
+      w.tmo = (ws & TMO_BIT) ? 1u : 0u;
+      w.ok = !w.tmo && (L.succ >= P.nruns || (L.past && L.ok));
+      w.wlim = L.Wn;
+    }
     __syncthreads();
   }
   }  // serial walk with repairs
-  // every run has exited: the ticket and the prologue flags start the next
-  // call at zero (no per-call memset; scratch is zeroed when allocated)
-  for (uint32_t r = tid; r < P.nruns; r += G::NT) P.flags[r] = 0;
+  // every run has exited: the ticket starts the next call at zero; the epoch
+  // word advances (the prologue flags of this call read as stale from now on)
   if (tid == 0) {
     P.head[0] = 0;
+    st_store(reinterpret_cast<uint64_t*>(P.head + HEAD_EPOCH), E);
     const uint64_t total = L.aux2;
     const cstate o = L.S;
     if (P.nframes) *P.nframes = total;
@@ -1688,20 +1854,33 @@ __global__ void k_stream_empty(const xyws_carry* cin, xyws_carry* cout, uint64_t
   }
 }
 
-constexpr uint64_t HEAD_BYTES = 512;  // [0] ticket, [1] error, [2..3] total; [64..128) carry; [128..384) stats
+constexpr uint64_t HEAD_BYTES = 512;  // [0] ticket, [1] error, [2..3] total, [4..5] epoch; [64..128) carry; [128..512) stats
+
+// hipFuncSetAttribute applies to the current device: once per (device,
+// geometry), under a lock (one process may drive several devices from several
+// threads).
+template <class G>
+int set_lds_attr() {
+  static std::mutex mu;
+  static bool done[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return XYWS_ERR_HIP;
+  std::lock_guard<std::mutex> lk(mu);
+  if (done[dev]) return XYWS_OK;
+  const int lds = (int)sizeof(lds_t<G>);
+  if (hipFuncSetAttribute((const void*)k_stream_runs<G>, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+          hipSuccess ||
+      hipFuncSetAttribute((const void*)k_stream_finish<G>, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+          hipSuccess)
+    return XYWS_ERR_HIP;
+  done[dev] = true;
+  return XYWS_OK;
+}
 
 template <class G>
 int launch_runs(const run_params& P, hipStream_t stream) {
-  static bool attr_set = false;
   const size_t lds = sizeof(lds_t<G>);
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)k_stream_runs<G>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess ||
-        hipFuncSetAttribute((const void*)k_stream_finish<G>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess)
-      return XYWS_ERR_HIP;
-    attr_set = true;
-  }
+  if (const int rc = set_lds_attr<G>()) return rc;
   hipLaunchKernelGGL(k_stream_runs<G>, dim3(P.nruns), dim3(G::NT), lds, stream, P);
   hipLaunchKernelGGL(k_stream_finish<G>, dim3(1), dim3(G::NT), lds, stream, P);
   if (P.frames && P.cap) hipLaunchKernelGGL(k_stream_emit, dim3(P.nruns), dim3(64), 0, stream, P);
@@ -1727,7 +1906,7 @@ void stream_scratch_free(stream_scratch* s) {
   s->max_runs = 0;
 }
 
-static uint64_t flags_bytes(uint64_t n) { return (4 * n + 255) & ~255ull; }
+static uint64_t flags_bytes(uint64_t n) { return (8 * n + 255) & ~255ull; }
 
 static int scratch_grow(stream_scratch* s, uint64_t runs) {
   if (s->mem && runs <= s->max_runs) return XYWS_OK;
@@ -1753,10 +1932,10 @@ int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
   return scratch_grow(s, nseg < maxr ? nseg + 1 : maxr);
 }
 
-int stream_scratch_stats(stream_scratch* s, uint64_t out[32]) {
+int stream_scratch_stats(stream_scratch* s, uint64_t out[XYWS_NSTATS]) {
   if (!s->mem) return XYWS_ERR_INVALID;
   if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
-  return hipMemcpy(out, static_cast<uint8_t*>(s->mem) + 128, 256, hipMemcpyDeviceToHost) == hipSuccess
+  return hipMemcpy(out, static_cast<uint8_t*>(s->mem) + 128, 8 * XYWS_NSTATS, hipMemcpyDeviceToHost) == hipSuccess
              ? XYWS_OK : XYWS_ERR_HIP;
 }
 
@@ -1768,10 +1947,11 @@ int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_ru
   return hipMemcpy(out, rec, n * R_WORDS * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int64_t)n : XYWS_ERR_HIP;
 }
 
-uint32_t stream_scratch_error(stream_scratch* s) {
+uint32_t stream_scratch_error(stream_scratch* s, bool clear) {
   if (!s->mem) return 0;
   uint32_t v[2] = {0, 0};
   if (hipMemcpy(v, s->mem, 8, hipMemcpyDeviceToHost) != hipSuccess) return 0xFFFFFFFFu;
+  if (clear && v[1] && hipMemset(static_cast<uint8_t*>(s->mem) + 4, 0, 4) != hipSuccess) return 0xFFFFFFFFu;
   return v[1];
 }
 
@@ -1811,13 +1991,13 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   P.nruns = (uint32_t)nruns;
   P.cout = cout; P.frames = frames; P.cap = cap; P.nframes = nframes;
   P.head = reinterpret_cast<uint32_t*>(m);
-  P.flags = reinterpret_cast<uint32_t*>(m + HEAD_BYTES);
+  P.flags = reinterpret_cast<uint64_t*>(m + HEAD_BYTES);
   P.rec = reinterpret_cast<uint64_t*>(m + HEAD_BYTES + flags_bytes(s->max_runs));
   P.opts = opts;
   // The ticket and the flags are zero here (zeroed at allocation, reset by
   // k_stream_finish after every call); the error word [1] is sticky until read
   // back. Run 0 snapshots the incoming carry into scratch.
-  if ((opts & XYWS_OPT_STATS) && hipMemsetAsync(m + 128, 0, 256, stream) != hipSuccess) return XYWS_ERR_HIP;
+  if ((opts & XYWS_OPT_STATS) && hipMemsetAsync(m + 128, 0, 8 * XYWS_NSTATS, stream) != hipSuccess) return XYWS_ERR_HIP;
   P.cin_user = cin;
   P.cin = reinterpret_cast<xyws_carry*>(m + 64);
   return small ? launch_runs<G_SMALL>(P, stream)

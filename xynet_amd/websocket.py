@@ -21,7 +21,7 @@ import enum
 import threading
 
 from . import _lib
-from ._lib import Carry, Frame, XywsError, check
+from ._lib import XYWS_OK, Carry, Frame, XywsError, check
 
 npos = (1 << 64) - 1
 
@@ -131,8 +131,12 @@ class Context:
         check(self.L.xyws_ctx_reserve(self.h, max_batch_bytes, max_frames), "xyws_ctx_reserve")
 
     def last_device_error(self):
+        """Device error word of the calls since the last read (0 = none);
+        synchronizes the device and clears the word (xyws.h)."""
         v = C.c_uint32()
-        check(self.L.xyws_ctx_last_device_error(self.h, C.byref(v)))
+        rc = self.L.xyws_ctx_last_device_error(self.h, C.byref(v))
+        if rc not in (XYWS_OK, _lib.XYWS_ERR_DEVICE):
+            check(rc, "xyws_ctx_last_device_error")
         return v.value
 
     def close(self):
@@ -219,15 +223,17 @@ class frame_decoder:
     back-to-back batches and unmask payloads in place, carrying a frame or header
     cut by a batch end into the next batch (xyws_decode_stream)."""
 
-    def __init__(self, device=None, serial=False, parse_only=False, small_segments=False):
+    def __init__(self, device=None, serial=False, parse_only=False, small_segments=False, opts=0, ctx=None):
         """serial: the one-lane exact chase (XYWS_OPT_SERIAL_SCAN). small_segments:
         test geometry of the run-parallel decoder (1 KiB runs), so that small
-        inputs cross many run boundaries (speculated entries and their repair)."""
+        inputs cross many run boundaries (speculated entries and their repair).
+        opts: further XYWS_OPT_* bits. ctx: a Context of its own (default: the
+        thread's context for the device)."""
         import torch
-        self.ctx = context(device)
+        self.ctx = ctx if ctx is not None else context(device)
         self.device = torch.device("cuda", self.ctx.device)
         self.carry_t = torch.zeros(64, dtype=torch.uint8, device=self.device)
-        self.opts = (4 if serial else 0) | (1 if parse_only else 0) | (0x200 if small_segments else 0)
+        self.opts = (4 if serial else 0) | (1 if parse_only else 0) | (0x200 if small_segments else 0) | opts
 
     def reset(self):
         self.carry_t.zero_()
