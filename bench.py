@@ -18,7 +18,9 @@ parity check after the timed region compares the device digest with the
 reference digest for that parity of step count (tests/golden/configs.json).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c1|c4]
-                       [--mode fused|serial] [--no-cpu] [--host-path]
+                       [--mode fused|serial] [--no-cpu] [--host-path] [--copies C] [--dry-run]
+--gpus N without a launcher starts N ranks (torch.distributed.run, one process
+per GPU) as a child process and passes their output through.
 """
 import argparse
 import ctypes as C
@@ -128,80 +130,172 @@ def device_digest(torch, T, buf):
     return int(out[0].item()) & ((1 << 64) - 1)
 
 
-def cpu_baseline(torch, buf, info, budget_s=12.0):
-    """Time the reference CPU path (oracle/_ref: the reference headers compiled
-    here) on a bounded host sample of the same batch. Returns a dict or None."""
+def cpu_threads():
+    """Host threads for the CPU baseline: the CPUs this process may run on
+    (sched_getaffinity), capped by OMP_NUM_THREADS when set (the GPU box sets
+    it to the box's CPU share; os.cpu_count() there shows the whole machine)."""
     try:
-        from oracle.oracle import Reference, Oracle, ref_lib_path
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline(torch, buf, info, budget_s=12.0):
+    """Time the CPU path on a bounded host sample of the same batch.
+
+    Primary (kind "port"): the committed C restatement of the reference hot
+    path (oracle/xyws_oracle.c, pinned to the reference's golden vectors) at
+    -O2 on all usable host threads: serial header walk + threaded unmask.
+    Beside it: the same at 1 thread, at -O0 (as the reference builds,
+    CMakeLists.txt:4), and the reference's own headers (oracle/_ref) when that
+    container-built library is present."""
+    try:
+        from oracle.oracle import Oracle, Reference, ref_lib_path, oracle_lib_path
     except Exception as e:  # pragma: no cover
         return {"error": f"oracle import failed: {e}"}
-    import numpy as np
     nframes, size = info["nframes"], info["size"]
     frame_bytes = size // max(nframes, 1)
-    sample_frames = max(1, min(nframes, (512 << 20) // max(frame_bytes, 1)))
-    sample_bytes = sample_frames * frame_bytes if info["golden"] != "c4_mixed" else min(size, 512 << 20)
+    if info["golden"] == "c4_mixed":
+        sample_bytes = min(size, 512 << 20)
+        payload_sample = int(info["payload_bytes"] * sample_bytes / size)
+    else:
+        sample_frames = max(1, min(nframes, (512 << 20) // max(frame_bytes, 1)))
+        sample_bytes = sample_frames * frame_bytes
+        payload_sample = sample_frames * (info["payload_bytes"] // max(nframes, 1))
     host = buf[:sample_bytes].cpu().numpy().copy()
-    threads = max(1, min(16, os.cpu_count() or 1))
-    kind = "reference" if os.path.exists(ref_lib_path("O2")) else "port"
-    res = {"kind": kind, "unit": "GiB/s",
-           "sample": f"first {sample_bytes} B of this rank's batch (host copy), whole frames only; "
-                     f"{'reference headers compiled -O2 (oracle/_ref)' if kind == 'reference' else 'oracle C restatement -O2'}"}
+    threads = cpu_threads()
 
-    def run(fn, nbytes_payload, budget):
+    def rate(fn, nbytes_payload, budget):
         reps, t0 = 0, time.perf_counter()
         while True:
             fn()
             reps += 1
             dt = time.perf_counter() - t0
             if dt >= budget:
-                return reps * nbytes_payload / dt / GIB
+                return round(reps * nbytes_payload / dt / GIB, 4)
 
-    payload_sample = sample_frames * (info["payload_bytes"] // max(nframes, 1))
-    if kind == "reference":
-        R = Reference("O2")
-        res["value"] = run(lambda: R.decode_batch_mt(host, threads), payload_sample, budget_s / 2)
-        res["cores"] = threads
-        res["value_1core"] = run(lambda: R.decode_batch_mt(host, 1), payload_sample, budget_s / 2)
+    small = host[: max(frame_bytes, min(host.size, 32 << 20) // max(frame_bytes, 1) * frame_bytes)].copy()
+    pay_small = int(payload_sample * small.size / max(host.size, 1))
+    O2 = Oracle()
+    res = {"kind": "port", "unit": "GiB/s", "cores": threads, "nproc": os.cpu_count(),
+           "sample": f"first {sample_bytes} B of this rank's batch (host copy, whole frames): "
+                     f"oracle/xyws_oracle.c restatement -O2, serial header walk + unmask on {threads} threads",
+           "value": rate(lambda: O2.decode_batch_mt(host, threads), payload_sample, budget_s * 0.4),
+           "value_1core": rate(lambda: O2.decode_batch_mt(host, 1), payload_sample, budget_s * 0.2)}
+    try:
+        O0 = Oracle(oracle_lib_path("O0"))
+        res["value_O0_1core"] = rate(lambda: O0.decode_batch_mt(small, 1), pay_small, budget_s * 0.1)
+    except Exception:
+        pass
+    if os.path.exists(ref_lib_path("O2")):  # the reference headers themselves (container-built)
         try:
-            R0 = Reference("O0")
-            small = host[: max(frame_bytes, min(host.size, 32 << 20) // frame_bytes * frame_bytes)].copy()
-            pay_small = (small.size // frame_bytes) * (info["payload_bytes"] // max(nframes, 1))
-            res["value_O0_1core"] = run(lambda: R0.decode_batch_mt(small, 1), pay_small, 2.0)
+            R = Reference("O2")
+            ref = {"value": rate(lambda: R.decode_batch_mt(host, threads), payload_sample, budget_s * 0.2),
+                   "cores": threads}
+            if os.path.exists(ref_lib_path("O0")):
+                R0 = Reference("O0")
+                ref["value_O0_1core"] = rate(lambda: R0.decode_batch_mt(small, 1), pay_small, budget_s * 0.1)
+            res["reference"] = ref
         except Exception:
             pass
-    else:
-        O = Oracle()
-        res["value"] = run(lambda: O.decode_stream(host, cap=16), payload_sample, budget_s)
-        res["cores"] = 1
     return res
 
 
-def host_path_rate(torch, ws, info, buf, chunk=256 << 20, reps=3):
-    """PCIe-inclusive rate for DESIGN.md: pinned host batch -> H2D -> decode -> D2H,
-    chunked over 3 streams (not the bench value)."""
+def host_path_rate(torch, ws, T, info, buf, golden, chunk=256 << 20, reps=3, nstreams=3):
+    """PCIe-inclusive rate for DESIGN.md (never the bench value): pinned host
+    batch -> H2D -> decode -> D2H, chunked at frame boundaries over `nstreams`
+    streams (one context: per-stream scratch). An odd number of passes leaves
+    the host batch decoded; its digest and the device error word are checked."""
     size = buf.numel()
     hostbuf = torch.empty(size, dtype=torch.uint8, pin_memory=True)
-    hostbuf.copy_(buf.cpu())
-    streams = [torch.cuda.Stream() for _ in range(3)]
-    devs = [torch.empty(chunk + (1 << 20), dtype=torch.uint8, device="cuda") for _ in range(3)]
-    decs = [ws.frame_decoder() for _ in range(3)]
-    # chunks cut at frame boundaries of the uniform batch (carry not needed)
+    hostbuf.copy_(buf.cpu())  # (buf holds the masked input batch)
+    streams = [torch.cuda.Stream() for _ in range(nstreams)]
+    devs = [torch.empty(chunk + (1 << 20), dtype=torch.uint8, device="cuda") for _ in range(nstreams)]
+    dec = ws.frame_decoder()
     fb = size // info["nframes"]
     per = max(1, chunk // fb) * fb
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
         for i, off in enumerate(range(0, size, per)):
-            k = i % 3
+            k = i % nstreams
             n = min(per, size - off)
             with torch.cuda.stream(streams[k]):
                 d = devs[k][:n]
                 d.copy_(hostbuf[off:off + n], non_blocking=True)
-                decs[k].decode(d, cap=0, count=False, carry=False)
+                dec.decode(d, cap=0, count=False, carry=False)
                 hostbuf[off:off + n].copy_(d, non_blocking=True)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return reps * info["payload_bytes"] / dt / GIB
+    err = dec.ctx.last_device_error()
+    # host digest of the result (odd reps: each chunk decoded an odd number of times)
+    chk = torch.empty(size, dtype=torch.uint8, device="cuda")
+    chk.copy_(hostbuf)
+    dig = device_digest(torch, T, chk)
+    want = golden["out_digest"] if reps % 2 == 1 else golden["in_digest"]
+    return {"gibs": round(reps * info["payload_bytes"] / dt / GIB, 3), "streams": nstreams,
+            "chunk_bytes": per, "passes": reps, "parity": dig == want and err == 0, "device_error": err}
+
+
+def source_hash():
+    """Hash of the decoder sources, stamped on PMC records (profiles/pmc_traffic.json)
+    so that a traffic figure is only reported for the kernel it was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("xyws_stream.hip", "xyws_device.h", "xyws_stream.h", "xyws.hip"):
+        with open(os.path.join(ROOT, "xynet_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(config, mode):
+    """HBM bytes per k_stream_runs launch from profiles/pmc_traffic.json when
+    that record was measured on these exact decoder sources; else None."""
+    pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(pmc_file):
+        return None, "no PMC record"
+    try:
+        rec = json.load(open(pmc_file)).get(config + ":" + mode)
+    except Exception:
+        return None, "unreadable PMC record"
+    if not rec:
+        return None, f"no PMC record for {config}:{mode}"
+    if rec.get("src_sha") != source_hash():
+        return None, f"PMC record {rec.get('src_sha')} is from other decoder sources ({source_hash()})"
+    return rec["hbm_bytes_per_launch"], f"profiles/pmc_traffic.json {config}:{mode} ({rec.get('profile', '?')})"
+
+
+def launch_ranks(args):
+    """--gpus N without a launcher: start N ranks with torch.distributed.run as
+    a CHILD process (nothing in this parent touches the GPU), pass their output
+    through, and exit with its status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def dry_run(world, rank):
+    """--dry-run: the N-rank plan without a GPU (gloo): every rank plans its
+    own shard; rank 0 prints the gathered plan (tests/test_multirank.py)."""
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    seed, gkey, desc = shard_plan("c3", rank, world)
+    plans = [None] * world
+    dist.all_gather_object(plans, {"rank": rank, "seed": seed, "golden": gkey})
+    t = max_over_ranks(dist, __import__("torch"), 1.0 + rank, "cpu")
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "shards": plans, "max_elapsed": t}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def main():
@@ -214,14 +308,22 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--host-path", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--copies", type=int, default=0,
+                    help="batch copies rotated over the steps (0: enough to exceed the 256 MiB Infinity Cache)")
+    ap.add_argument("--dry-run", action="store_true", help="plan the N-rank run on the CPU (gloo) and exit")
     ap.add_argument("--stats", action="store_true", help="print fused-decoder resolution counters")
     ap.add_argument("--xopts", type=lambda x: int(x, 0), default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
-    import torch
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(world, rank)
+
+    import torch
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -230,18 +332,26 @@ def main():
 
     from xynet_amd import _lib, websocket as ws
     T = _lib.load_tools()
-    buf, info = build_batch(torch, T, args.config, rank, world)
+    buf0, info = build_batch(torch, T, args.config, rank, world)
     golden = load_golden().get(info["golden"])
+    # Batches below the 256 MiB Infinity Cache (c1, c2) are timed over >= 4
+    # copies used in turn, so that each step reads its batch from HBM
+    # (SURVEY.md §7); every copy's parity is checked.
+    ncopies = args.copies or (1 if info["size"] >= (1 << 30) else max(4, -(-(1 << 30) // info["size"])))
+    bufs = [buf0] + [buf0.clone() for _ in range(ncopies - 1)]
+    uses = [0] * ncopies
     dec = ws.frame_decoder(serial=(args.mode == "serial"))
     dec.opts |= args.xopts
-    dec.ctx.reserve(buf.numel(), 0)
+    dec.ctx.reserve(info["size"], 0)
     stream = torch.cuda.current_stream()
 
-    def step():  # fresh stream each step: no carry in/out, no frame table, no count
-        dec.decode(buf, cap=0, count=False, carry=False)
+    def step(i):  # fresh stream each step: no carry in/out, no frame table, no count
+        k = i % ncopies
+        uses[k] += 1
+        dec.decode(bufs[k], cap=0, count=False, carry=False)
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(i)
     torch.cuda.synchronize()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -252,9 +362,10 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         evs[i][0].record(stream)
-        dec.decode(buf, cap=0, count=False, carry=False)
+        step(args.warmup + i)
         evs[i][1].record(stream)
     torch.cuda.synchronize()
+    t_own = time.perf_counter() - t0
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
@@ -262,64 +373,59 @@ def main():
     kernel_ms = sorted(a.elapsed_time(b) for a, b in evs)
     avg_ms = sum(kernel_ms) / len(kernel_ms)
 
-    if args.stats and rank == 0:  # one extra counted decode pair (keeps the step parity)
+    if args.stats and rank == 0:  # two extra decodes of copy 0 (keeps its parity)
         names = ["runs", "runs_without_entry", "bad_boundaries", "repairs", "cuts", "spins", "dense_passes",
                  "frames", "scan_segments", "scan_survivors", "scan_undecided", "cyc_scan_filter",
                  "cyc_scan_check", "cyc_scan_resolve", "cyc_dense_entry", "cyc_dense_chase", "cyc_prologue", "cyc_main", "cyc_wait",
                  "cyc_fill", "cyc_chase_sync", "cyc_xor", "cyc_tail", "cyc_prefetch_issue", "cyc_chase_pass",
                  "cyc_pro_fill", "cyc_pro_scan", "cyc_pro_publish", "dense_no_entry", "dense_chase_fail",
-                 "dense_mismatch", "dense_overflow", "giveups", "bridges", "-"]
+                 "dense_mismatch", "dense_overflow", "giveups", "bridges"]
         for _ in range(2):
             dec.opts |= _lib.OPT_STATS
-            dec.decode(buf, cap=0, count=False, carry=False)
+            dec.decode(bufs[0], cap=0, count=False, carry=False)
             dec.opts &= ~_lib.OPT_STATS
             out = (C.c_uint64 * _lib.NSTATS)()
             dec.ctx.L.xyws_debug_stats(dec.ctx.h, C.c_void_p(stream.cuda_stream), out)
-        st = {k: v for k, v in zip(names, list(out)) if k != "-"}
+        st = {k: v for k, v in zip(names, list(out))}
         nrun = max(1, st["runs"] + 1)
         for k in list(st):
             if k.startswith("cyc_"):
                 st[k.replace("cyc_", "us_per_run_")] = round(st.pop(k) / nrun / 2100.0, 3)
         print(json.dumps({"stats": st}), flush=True)
 
-    # parity after the timed region: total decodes = warmup + steps
+    # parity after the timed region: every copy against the reference digest
+    # for the parity of its decode count (XOR is an involution)
     dev_err = dec.ctx.last_device_error()
-    dig = device_digest(torch, T, buf)
-    odd = (args.warmup + args.steps) % 2 == 1
     parity = None
     if golden is not None:
-        parity = (dig == (golden["out_digest"] if odd else golden["in_digest"])) and dev_err == 0
+        parity = dev_err == 0
+        for b, u in zip(bufs, uses):
+            parity = parity and device_digest(torch, T, b) == (golden["out_digest"] if u % 2 else golden["in_digest"])
 
+    per_gpu = args.steps * info["payload_bytes"] / t_own / GIB
+    per_gpu_all = [per_gpu]
+    if dist:
+        per_gpu_all = [None] * world
+        dist.all_gather_object(per_gpu_all, round(per_gpu, 3))
     total_payload = info["payload_bytes"] * world
     value = args.steps * total_payload / elapsed / GIB
     achieved = info["algo_bytes"] / (avg_ms * 1e-3) / 1e9
-
-    parities = [all_ranks(dist, torch, parity, "cuda") if dist else parity]
+    parity_all = all_ranks(dist, torch, parity, "cuda") if dist else parity
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        # sample taken from a masked-state batch: regenerate if an odd count was applied
-        if odd:
-            step()
-            torch.cuda.synchronize()
-        cpu = cpu_baseline(torch, buf, info, args.cpu_budget)
-        if odd:
-            step()
-            torch.cuda.synchronize()
     host_rate = None
-    if args.host_path and rank == 0 and info["nframes"] and args.config != "c4":
-        host_rate = host_path_rate(torch, ws, info, buf)
+    if rank == 0 and world == 1 and (not args.no_cpu or args.host_path):
+        # both legs take the masked input batch: decode copy 0 once more if it is unmasked
+        if uses[0] % 2:
+            dec.decode(bufs[0], cap=0, count=False, carry=False)
+            uses[0] += 1
+            torch.cuda.synchronize()
+        if not args.no_cpu:
+            cpu = cpu_baseline(torch, bufs[0], info, args.cpu_budget)
+        if args.host_path and info["nframes"] and args.config != "c4" and golden is not None:
+            host_rate = host_path_rate(torch, ws, T, info, bufs[0], golden)
 
-    traffic = None
-    pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_file):
-        try:
-            pm = json.load(open(pmc_file))
-            rec = pm.get(args.config + ":" + args.mode)
-            if rec:
-                traffic = rec["hbm_bytes_per_launch"]
-        except Exception:
-            traffic = None
+    traffic, traffic_src = pmc_traffic(args.config, args.mode)
 
     if rank == 0:
         line = {
@@ -341,8 +447,10 @@ def main():
                 "frames_per_gpu": info["nframes"],
                 "batch_bytes_per_gpu": info["size"],
                 "payload_bytes_per_gpu": info["payload_bytes"],
+                "batch_copies": ncopies,
                 "parallelism": f"shard-by-frame x{world}, no collective",
             },
+            "per_gpu_gibs": per_gpu_all,
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
@@ -350,15 +458,17 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": info["algo_bytes"],
                 "kernel_ms_avg": round(avg_ms, 4),
                 "kernel_ms_min": round(kernel_ms[0], 4),
+                "src_sha": source_hash(),
             },
             "cpu_baseline": cpu,
-            "parity": bool(parities[0]) if parities[0] is not None else None,
+            "parity": bool(parity_all) if parity_all is not None else None,
         }
         if host_rate is not None:
-            line["host_path_gibs"] = round(host_rate, 3)
+            line["host_path"] = host_rate
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

@@ -63,9 +63,13 @@ def build(quiet=True):
         print(out.stdout)
 
 
+def oracle_lib_path(opt="O2"):
+    return os.path.join(HERE, "liboracle.so" if opt == "O2" else "liboracle_O0.so")
+
+
 class Oracle:
     def __init__(self, path=None):
-        path = path or os.path.join(HERE, "liboracle.so")
+        path = path or oracle_lib_path("O2")
         if not os.path.exists(path):
             build()
         L = self.L = C.CDLL(path)
@@ -94,6 +98,8 @@ class Oracle:
         L.oracle_mixed_table.restype = u64
         L.oracle_mixed_table.argtypes = [u64, u64, vp, u64, C.POINTER(u64)]
         L.oracle_fill_mixed.argtypes = [vp, vp, u64, u64]
+        L.oracle_decode_batch_mt.restype = u64
+        L.oracle_decode_batch_mt.argtypes = [vp, u64, C.c_int]
 
     # --- parser object (websocket_frame_header_parser) ---
     class Parser:
@@ -155,6 +161,10 @@ class Oracle:
 
     def digest(self, buf: np.ndarray) -> int:
         return self.L.oracle_digest(_ptr(buf), buf.size)
+
+    def decode_batch_mt(self, buf: np.ndarray, threads: int) -> int:
+        """The CPU baseline: serial header walk, threaded unmask (whole frames)."""
+        return self.L.oracle_decode_batch_mt(_ptr(buf), buf.size, threads)
 
     def frames_digest(self, raw: np.ndarray) -> int:
         """Digest of a descriptor table (xyws_frame records as raw bytes): the

@@ -26,8 +26,10 @@
  * against the reference's own test cases (test/websocket_frame_test.cpp:10-89)
  * and the RFC 6455 §5.7 "Hello" example.
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <stdlib.h>
 #include <string.h>
 #include "xyws.h"
 #include "xyws_synth.h"
@@ -345,4 +347,64 @@ void oracle_fill_mixed(uint8_t* buf, const xyws_synth_frame* tab, uint64_t n, ui
     for (uint64_t j = 0; j < fr->plen; j++)
       pl[j] = xyws_synth_plain_byte(seed, fr->draw, j) ^ (uint8_t)(key >> (8 * (j & 3)));
   }
+}
+
+/* ---- CPU baseline (bench.py cpu_baseline, kind "port") --------------------
+ * The reference's per-frame work on a batch held in host memory, on `threads`
+ * host threads: one thread walks the headers with the parser above (boundary
+ * discovery is serial by nature: websocket_frame_header.h:305-385), then the
+ * frames' payloads are unmasked with oracle_mask (websocket_frame_mask.h:6-25)
+ * by `threads` workers over byte-balanced contiguous frame ranges. Whole
+ * frames only (a trailing partial frame is ignored). Returns the frame count. */
+typedef struct { uint64_t ps, plen; uint32_t mask; } oracle_span;
+typedef struct { uint8_t* buf; const oracle_span* fs; uint64_t a, b; } oracle_work;
+
+static void* oracle_worker(void* arg) {
+  const oracle_work* w = (const oracle_work*)arg;
+  for (uint64_t i = w->a; i < w->b; i++) oracle_mask(w->buf + w->fs[i].ps, w->fs[i].plen, w->fs[i].mask, 0);
+  return NULL;
+}
+
+uint64_t oracle_decode_batch_mt(uint8_t* buf, uint64_t len, int threads) {
+  uint64_t cap = 1024, n = 0, pos = 0;
+  oracle_span* fs = (oracle_span*)malloc(cap * sizeof *fs);
+  if (!fs) return 0;
+  while (pos < len) {
+    oracle_parser p;
+    oracle_parser_reset(&p);
+    size_t r = oracle_parser_parse(&p, buf + pos, len - pos);
+    if (r == ORACLE_NPOS || p.length > len - (pos + r)) break;
+    if (n == cap) {
+      oracle_span* g = (oracle_span*)realloc(fs, 2 * cap * sizeof *fs);
+      if (!g) break;
+      fs = g;
+      cap *= 2;
+    }
+    fs[n].ps = pos + r;
+    fs[n].plen = p.length;
+    fs[n].mask = oracle_parser_mask_u32(&p);
+    n++;
+    pos += r + p.length;
+  }
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t tid[256];
+  oracle_work w[256];
+  uint64_t per = pos / (uint64_t)threads + 1, a = 0;
+  int nt = 0;
+  for (int t = 0; t < threads && a < n; t++) {
+    uint64_t b = a, lim = (uint64_t)(t + 1) * per;
+    while (b < n && (fs[b].ps < lim || b == a)) b++;
+    if (t == threads - 1) b = n;
+    w[nt].buf = buf; w[nt].fs = fs; w[nt].a = a; w[nt].b = b;
+    if (threads == 1 || pthread_create(&tid[nt], NULL, oracle_worker, &w[nt]) != 0) {
+      oracle_worker(&w[nt]);
+    } else {
+      nt++;
+    }
+    a = b;
+  }
+  for (int t = 0; t < nt; t++) pthread_join(tid[t], NULL);
+  free(fs);
+  return n;
 }

@@ -57,3 +57,24 @@ def test_single_rank_plan_is_config3():
     seed, gkey, _ = bench.shard_plan("c3", 0, 1)
     assert (seed, gkey) == (0x5EED0003, "c3_bin_64k")
     assert bench.max_over_ranks(None, torch, 3.5, "cpu") == 3.5
+
+
+def test_bench_gpus2_launches_two_ranks_dry_run():
+    """`bench.py --gpus 2` without a launcher starts 2 ranks itself
+    (torch.distributed.run child process); --dry-run plans them on the CPU
+    (gloo): rank 0 reports n_gpus = 2 and two disjoint shard plans."""
+    import subprocess
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["dry_run"] is True and out["n_gpus"] == 2
+    seeds = sorted(p["seed"] for p in out["shards"])
+    assert seeds == [0x5EED0005, 0x5EED0006]
+    assert sorted(p["golden"] for p in out["shards"]) == ["c5_shard0", "c5_shard1"]
+    assert out["max_elapsed"] == 2.0
