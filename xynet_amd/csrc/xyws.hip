@@ -278,16 +278,13 @@ __global__ void __launch_bounds__(UNMASK_THREADS) k_unmask_tiles(uint8_t* __rest
 // and frame table belong to the stream it was enqueued on, so calls on one
 // context from several streams (an io_uring service overlapping batches) run
 // concurrently without sharing scratch. XYWS_SLOTS streams get a slot each;
-// a further stream takes the least recently used slot after waiting (on the
-// device, hipStreamWaitEvent) for that slot's last call.
-#define XYWS_SLOTS 8
+// when a further stream arrives while every slot is bound, the device is
+// synchronized (every slot idle) and the bindings start over.
+#define XYWS_SLOTS 16
 
 struct scratch_slot {
   bool bound;
   hipStream_t stream;
-  uint64_t last_use;
-  hipEvent_t ev;      // recorded after the slot's last call (not while capturing)
-  bool ev_valid;
   // frame table scratch (indexed + serial modes)
   void* tab_mem;
   uint64_t tab_cap;
@@ -298,7 +295,6 @@ struct xyws_ctx {
   int device;
   std::mutex mu;
   uint32_t* err;  // device error word (serial / indexed modes)
-  uint64_t clock;
   uint64_t reserve_bytes, reserve_frames;  // applied to every slot
   scratch_slot slot[XYWS_SLOTS];
 };
@@ -364,30 +360,21 @@ int acquire_slot(xyws_ctx* ctx, hipStream_t stream, bool capture, scratch_slot**
   scratch_slot* pick = nullptr;
   for (auto& sl : ctx->slot)
     if (sl.bound && sl.stream == stream) { pick = &sl; break; }
-  if (!pick)
+  if (!pick) {
+    bool any_free = false;
+    for (auto& sl : ctx->slot) any_free = any_free || !sl.bound;
+    if (!any_free) {
+      // every slot bound to another stream: wait until all of them are idle
+      if (capture) return XYWS_ERR_CAPACITY;
+      if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
+      for (auto& sl : ctx->slot) sl.bound = false;
+    }
     for (auto& sl : ctx->slot)
       if (!sl.bound) { pick = &sl; break; }
-  if (!pick) {
-    for (auto& sl : ctx->slot)
-      if (!pick || sl.last_use < pick->last_use) pick = &sl;
-    if (pick->ev_valid) {
-      if (capture) return XYWS_ERR_CAPACITY;  // (an event from outside the capture)
-      if (hipStreamWaitEvent(stream, pick->ev, 0) != hipSuccess) return XYWS_ERR_HIP;
-    }
   }
   pick->bound = true;
   pick->stream = stream;
-  pick->last_use = ++ctx->clock;
   *out = pick;
-  return XYWS_OK;
-}
-
-// After enqueueing a call on the slot: its completion event.
-int release_slot(scratch_slot* sl, hipStream_t stream, bool capture) {
-  if (capture) return XYWS_OK;
-  if (!sl->ev && hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming) != hipSuccess) return XYWS_ERR_HIP;
-  if (hipEventRecord(sl->ev, stream) != hipSuccess) return XYWS_ERR_HIP;
-  sl->ev_valid = true;
   return XYWS_OK;
 }
 
@@ -420,15 +407,11 @@ int xyws_ctx_create(int device, xyws_ctx** out) {
   xyws_ctx* c = new xyws_ctx();
   c->device = device;
   c->err = nullptr;
-  c->clock = 0;
   c->reserve_bytes = 0;
   c->reserve_frames = 0;
   for (auto& sl : c->slot) {
     sl.bound = false;
     sl.stream = nullptr;
-    sl.last_use = 0;
-    sl.ev = nullptr;
-    sl.ev_valid = false;
     sl.tab_mem = nullptr;
     sl.tab_cap = 0;
     stream_scratch_init(&sl.ss, device);
@@ -453,7 +436,6 @@ int xyws_ctx_destroy(xyws_ctx* ctx) {
     (void)hipDeviceSynchronize();
     for (auto& sl : ctx->slot) {
       if (sl.tab_mem) (void)hipFree(sl.tab_mem);
-      if (sl.ev) (void)hipEventDestroy(sl.ev);
       stream_scratch_free(&sl.ss);
     }
     if (ctx->err) (void)hipFree(ctx->err);
@@ -564,14 +546,14 @@ int xyws_decode_indexed(xyws_ctx* ctx, void* dev_buf, uint64_t len, const uint64
                        base, lo, hi, t);
     if ((rc = hip_err(hipGetLastError()))) return rc;
   }
-  return release_slot(sl, s, cap);
+  return XYWS_OK;
 }
 
 int xyws_decode_stream(xyws_ctx* ctx, void* dev_buf, uint64_t len, const xyws_carry* dev_carry_in,
                        xyws_carry* dev_carry_out, xyws_frame* dev_frames, uint64_t cap,
                        uint64_t* dev_nframes, uint32_t opts, void* stream) {
   if (!ctx || (!dev_buf && len)) return XYWS_ERR_INVALID;
-  if (len >= (1ull << 46)) return XYWS_ERR_INVALID;
+  if (len >= (1ull << 46) - 64) return XYWS_ERR_INVALID;  // (entry granules hold 46-bit positions)
   std::lock_guard<std::mutex> lk(ctx->mu);
   device_guard g(ctx->device);
   if (!g.ok) return XYWS_ERR_HIP;
@@ -599,12 +581,10 @@ int xyws_decode_stream(xyws_ctx* ctx, void* dev_buf, uint64_t len, const xyws_ca
                          base, lo, hi, t);
       if ((rc = hip_err(hipGetLastError()))) return rc;
     }
-    return release_slot(sl, s, capt);
+    return XYWS_OK;
   }
-  rc = stream_decode_fused(&sl->ss, base, lo, hi, dev_carry_in, dev_carry_out, dev_frames, cap,
-                           dev_nframes, opts, s);
-  if (rc) return rc;
-  return release_slot(sl, s, capt);
+  return stream_decode_fused(&sl->ss, base, lo, hi, dev_carry_in, dev_carry_out, dev_frames, cap,
+                             dev_nframes, opts, s);
 }
 
 }  // extern "C"

@@ -136,15 +136,38 @@ enum {
 // R_OK bits
 constexpr uint64_t OK_BIT = 1, TMO_BIT = 2;  // chain landed on the successor; successor wait timed out
 
-// Prologue flags, one u64 per run, stamped with the call's epoch E (head word
-// HEAD_EPOCH holds the number of completed calls; a call runs with E = that +
-// 1): (E << 1) = claimed in this call (by the run's own workgroup),
-// (E << 1) | 1 = published. Anything below E << 1 is a previous call's and
-// reads as unclaimed, so no per-call reset is needed and a stale record is
-// never taken for a live one.
+// Entry granules, 16 bytes per run, each written by ONE 16-byte sc1 store and
+// read by ONE 16-byte sc1 load (MI355X_MICROARCH.md §inter-workgroup
+// visibility: 16-B granules observed untorn), stamped with the call's epoch E
+// (head word HEAD_EPOCH holds the number of completed calls; a call runs with
+// E = that + 1):
+//   word 0: (E << 1) = claimed by the run's own workgroup in this call,
+//           (E << 1) | 1 = published; anything below E << 1 is a previous
+//           call's and reads as unclaimed (no per-call reset, no stale record);
+//   word 1 (published): h (46 bits, G_NONE = no entry) | (W - h) << 46 (5
+//           bits: W = round16(h + header)) | (E mod 2^13) << 51, the tag a
+//           torn read would fail.
+// The run's record (R_H, R_W, entry state, ...) is for k_stream_finish only,
+// so the publish needs no wait for the record stores (nor for the prefetch
+// loads in flight).
 XYWS_DEV uint64_t flag_claimed(uint64_t E) { return E << 1; }
 XYWS_DEV uint64_t flag_published(uint64_t E) { return (E << 1) | 1u; }
-constexpr uint32_t HEAD_EPOCH = 4;  // u32 index of the u64 epoch word in head[]
+constexpr uint64_t G_NONE = (1ull << 46) - 1;
+XYWS_DEV uint64_t granule_tag(uint64_t E) { return (E & 0x1FFFull) << 51; }
+constexpr uint32_t HEAD_EPOCH = 4;   // u32 index of the u64 epoch word in head[]
+constexpr uint32_t HEAD_DONE = 6;    // u32: runs finished in this call (the last one finishes the call)
+constexpr uint32_t HEAD_REPAIR = 7;  // u32: the fast finish found a bad hand-off (k_stream_finish walks)
+
+XYWS_DEV void granule_store(uint64_t* g, uint64_t a, uint64_t b) {
+  const u32x4 v = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(g), "v"(v) : "memory");
+}
+XYWS_DEV void granule_load(const uint64_t* g, uint64_t& a, uint64_t& b) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(g) : "memory");
+  a = (uint64_t)v.x | ((uint64_t)v.y << 32);
+  b = (uint64_t)v.z | ((uint64_t)v.w << 32);
+}
 
 struct run_params {
   uint8_t* base;
@@ -158,8 +181,9 @@ struct run_params {
   uint64_t cap;
   uint64_t* nframes;
   uint64_t* rec;          // R_WORDS per run
-  uint64_t* flags;        // per run: prologue claim/publish word (epoch-stamped, see flag_claimed)
-  uint32_t* head;         // [0] ticket, [1] error word, [2..3] u64 total, [4..5] u64 epoch; stats at [32..)
+  uint64_t* flags;        // per run: entry granule (2 x u64, see flag_claimed)
+  uint32_t* head;         // [0] ticket, [1] error word, [2..3] u64 total, [4..5] u64 epoch, [6] done,
+                          // [7] repair; [16..32) carry snapshot; stats at [32..)
   uint32_t opts;
 };
 
@@ -199,7 +223,6 @@ XYWS_DEV void st_store(uint64_t* p, uint64_t v) {
 XYWS_DEV uint64_t st_load(const uint64_t* p) {
   return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-XYWS_DEV uint64_t flag_load(const uint64_t* p) { return st_load(p); }
 XYWS_DEV bool stats_on(const run_params& P) { return (P.opts & XYWS_OPT_STATS) != 0; }
 enum { ST_RUNS = 0, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRAMES,
        ST_P_WIN, ST_P_CAND, ST_P_UND, ST_P_TCOMP, ST_P_TCHECK, ST_P_TRES, ST_D_TENT, ST_D_TCHASE,
@@ -761,10 +784,9 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   {
     const uint32_t s = tid / SECT, j = tid % SECT, skip = L.dent[s];
     const bool mv = j >= skip && j < L.dcnt[s];
-    fent e;
-    if (mv) e = L.fl[tid];
+    const u32x4 e = mv ? *reinterpret_cast<const u32x4*>(&L.fl[tid]) : u32x4{0u, 0u, 0u, 0u};
     __syncthreads();
-    if (mv) L.fl[L.doff[s] + j - skip] = e;
+    if (mv) *reinterpret_cast<u32x4*>(&L.fl[L.doff[s] + j - skip]) = e;
   }
   if (tid == 0) {
     if (cover) {
@@ -826,18 +848,21 @@ XYWS_DEV void build_rows(lds_t<G>& L, uint32_t nfl, uint32_t lo_c, uint32_t hi_c
   }
 }
 
-// Wait until run j's prologue, claimed in this call, is published (lane 0).
-// The claimer is run j's own running workgroup, which computes the prologue
-// without waiting for anything, so the wait ends; the bound only reports a bug.
-XYWS_DEV bool wait_published(const run_params& P, uint32_t j, uint64_t E) {
+// Wait until run j's entry granule, claimed in this call, is published (lane
+// 0); false when the bounded wait timed out (reported). The claimer is run j's
+// own running workgroup, which computes its prologue without waiting for
+// anything, so the wait ends; the bound only reports a bug.
+XYWS_DEV bool wait_published(const run_params& P, uint32_t j, uint64_t E, uint64_t& a, uint64_t& b) {
   const uint64_t want = flag_published(E);
   uint32_t it = 0;
-  while (flag_load(P.flags + j) != want && it < SPIN) {
+  for (;;) {
+    granule_load(P.flags + 2 * (uint64_t)j, a, b);
+    if (a == want || it >= SPIN) break;
     __builtin_amdgcn_s_sleep(2);
     it++;
   }
   if (it) stat_add(P, ST_SPIN, it);
-  if (it >= SPIN) {
+  if (a != want) {
     atomicOr(P.head + 1, 2u);
     return false;
   }
@@ -846,12 +871,11 @@ XYWS_DEV bool wait_published(const run_params& P, uint32_t j, uint64_t E) {
 
 // The next run after `run` that has an entry (lane 0), starting the search at
 // L.scan_j. Returns LK_FOUND with (hn, Wn, succ) (succ = nruns: none), or
-// LK_GIVEUP with succ = the run whose prologue is not published: its workgroup
+// LK_GIVEUP with succ = the run whose entry is not published: its workgroup
 // has not started (not every workgroup of the grid is resident, e.g. beside a
 // concurrent decode, and waiting for one that is not could deadlock), or its
-// bounded wait timed out (reported in the error word). Never reads a record
-// whose flag is not published in this call. A run given up on is bridged by
-// k_stream_finish.
+// bounded wait timed out (reported in the error word). Never uses a granule
+// not published in this call. A run given up on is bridged by k_stream_finish.
 enum { LK_FOUND = 0, LK_GIVEUP = 1 };
 template <class G>
 XYWS_DEV uint32_t lookup_successor(const run_params& P, lds_t<G>& L, uint64_t& hn, uint64_t& Wn, uint64_t& succ,
@@ -859,16 +883,20 @@ XYWS_DEV uint32_t lookup_successor(const run_params& P, lds_t<G>& L, uint64_t& h
   const uint64_t E = L.E;
   for (uint64_t j = L.scan_j; j < P.nruns; j++) {
     L.scan_j = j;
+    uint64_t a, b;
+    granule_load(P.flags + 2 * j, a, b);
     // (test mode: odd runs give up on their successor at once)
     const bool test = (P.opts & XYWS_OPT_TEST_GIVEUP) && (run & 1u);
-    if (test || (flag_load(P.flags + j) >> 1) < E || !wait_published(P, (uint32_t)j, E)) {
+    if (test || (a >> 1) < E || (a != flag_published(E) && !wait_published(P, (uint32_t)j, E, a, b)) ||
+        (b & (0x1FFFull << 51)) != granule_tag(E)) {
+      if (a == flag_published(E) && (b & (0x1FFFull << 51)) != granule_tag(E)) atomicOr(P.head + 1, 8u);
       succ = j;
       return LK_GIVEUP;
     }
-    const uint64_t h = st_load(P.rec + j * R_WORDS + R_H);
-    if (h != NONE) {
+    const uint64_t h = b & G_NONE;
+    if (h != G_NONE) {
       hn = h;
-      Wn = st_load(P.rec + j * R_WORDS + R_W);
+      Wn = h + ((b >> 46) & 31u);
       succ = j;
       return LK_FOUND;
     }
@@ -1409,8 +1437,8 @@ XYWS_DEV void prologue(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t
     st_store(rec + R_W, W);
     put_state(rec + R_S0, S);
     st_store(rec + R_HEAD, hc);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(P.flags + run, flag_published(L.E), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    granule_store(P.flags + 2 * (uint64_t)run, flag_published(L.E),
+                  (h == NONE ? G_NONE : (h | ((W - h) << 46))) | granule_tag(L.E));
     L.S = S;
     L.cnt = hc;
     // dense-pass hint for the first segment: the entry's frame is small
@@ -1424,137 +1452,53 @@ XYWS_DEV void prologue(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t
   __syncthreads();
 }
 
-// ---------------------------------------------------------------- kernels
-template <class G>
-__global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
-  lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
-  const uint32_t tid = threadIdx.x;
-  if (tid == 0) {
-    L.ticket = atomicAdd(P.head, 1u);
-    L.E = st_load(reinterpret_cast<const uint64_t*>(P.head + HEAD_EPOCH)) + 1;
-  }
-  __syncthreads();
-  const uint32_t run = uniform32(L.ticket);
-  if (run >= P.nruns) return;
-  uint64_t* rec = P.rec + (uint64_t)run * R_WORDS;
-  if (tid == 0) st_store(rec + R_ECNT, 0);  // no descriptors unless k_stream_finish plans them
-  const uint64_t rng_end = run + 1 < P.nruns ? (uint64_t)(run + 1) * P.rbytes : NONE;
-  seg_io<G> io;
-  uint64_t wlo, ss0;
-  bool in_lds = false;
-  if (run == 0) {
-    if (tid == 0) {
-      // snapshot of the incoming carry for k_stream_finish / k_stream_emit
-      // (the caller's carry may alias the carry out, which finish writes)
-      xyws_carry cz;
-      if (P.cin_user) {
-        cz = *P.cin_user;
-      } else {
-        for (int i = 0; i < 64; i++) reinterpret_cast<uint8_t*>(&cz)[i] = 0;
-      }
-      *P.cin = cz;
-      uint64_t c0;
-      L.S = initial_state(P, &cz, c0);
-      L.cnt = c0;
-      st_store(rec + R_H, P.lo);
-      st_store(rec + R_W, P.lo);
-      put_state(rec + R_S0, L.S);
-      st_store(rec + R_HEAD, c0);
+// The call's outputs (lane 0): frame count, total, carry out. cin: the
+// incoming-carry snapshot, o: the final chain state.
+XYWS_DEV void write_outputs(const run_params& P, const xyws_carry& cin, uint64_t total, const cstate& o) {
+  if (P.nframes) *P.nframes = total;
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(P.head + 2), total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!P.cout) return;
+  const uint64_t lo = P.lo, hi = P.hi;
+  xyws_carry c;
+  for (int i = 0; i < 64; i++) reinterpret_cast<uint8_t*>(&c)[i] = 0;
+  c.frames_total = cin.frames_total + total;
+  if (o.st & S_PARTIAL) {
+    uint32_t nb = 0;
+    if (o.st & S_PARTCARRY) {
+      for (; nb < cin.hdr_len; nb++) c.hdr[nb] = cin.hdr[nb];
+      for (uint64_t q = lo; q < hi && nb < 14; q++) c.hdr[nb++] = P.base[q];
+    } else {
+      for (uint64_t q = o.X; q < hi && nb < 14; q++) c.hdr[nb++] = P.base[q];
     }
-    wlo = P.lo;
-    ss0 = 0;
-  } else {
-    // claim the own prologue (a predecessor that finds it unclaimed gives up
-    // on this run instead of waiting for a workgroup that may not be running)
-    if (tid == 0)
-      __hip_atomic_store(P.flags + run, flag_claimed(L.E), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    prologue<G>(P, L, io, tid, run);
-    if (L.aux2 == NONE) return;  // no entry: the chain of an earlier run covers this range
-    wlo = uniform64(L.aux2);
-    // the chain starts in the scanned segment (usual) or on the grid after it
-    const uint64_t a1 = uniform64(L.aux1);
-    ss0 = a1 + (wlo - a1) / G::SEG * G::SEG;
-    in_lds = ss0 == a1;
-    // (the next segment's loads were issued before the scan)
-    if (in_lds && ss0 + G::SEG < P.hi && io.pf != ss0 + G::SEG) io.issue(P, ss0 + G::SEG, tid);
+    c.hdr_len = (uint8_t)nb;
+  } else if (o.X > hi && !(o.st & S_NOCOV)) {
+    if (o.st & S_CARRIED) {
+      c.payload_remaining = cin.payload_remaining - (hi - lo);
+      c.phase = cin.phase + (hi - lo);
+      for (int i = 0; i < 4; i++) c.key[i] = cin.key[i];
+    } else {
+      const hdr_info hh = (o.st & S_HDRCARRY) ? header_carried(P, &cin) : hdr_global(P, o.cov_start, NONE);
+      c.payload_remaining = hh.plen - (hi - o.cov_ps);
+      c.phase = hi - o.cov_ps;
+      c.key[0] = (uint8_t)hh.key; c.key[1] = (uint8_t)(hh.key >> 8);
+      c.key[2] = (uint8_t)(hh.key >> 16); c.key[3] = (uint8_t)(hh.key >> 24);
+    }
   }
-  if (tid == 0) {
-    L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.tmo = 0; L.first_after = NONE;
-    if (run == 0) L.dense = 0;
-    L.known = rng_end == NONE;
-    L.hn = NONE; L.Wn = NONE; L.succ = P.nruns; L.scan_j = run + 1;
-  }
-  __syncthreads();
-  uint64_t t1 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
-  run_chain(P, L, io, tid, ss0, in_lds, wlo, rng_end, run);
-  if (tid == 0) {
-    uint64_t* rec = P.rec + (uint64_t)run * R_WORDS;
-    const bool ok = !L.tmo && (L.succ >= P.nruns || (L.past && L.ok));
-    st_store(rec + R_OK, (ok ? OK_BIT : 0) | (L.tmo ? TMO_BIT : 0) | ((uint64_t)L.succ << 32));
-    st_store(rec + R_HN, L.hn);
-    st_store(rec + R_WN, L.Wn);
-    st_store(rec + R_CNT, L.cnt);
-    st_store(rec + R_TAIL, L.tail);
-    st_store(rec + R_FIRST, L.first_after);
-    put_state(rec + R_F0, L.S);
-    st_store(rec + R_EP, L.E);
-    if (!ok) stat_add(P, ST_BAD, 1);
-    if (L.tmo) stat_add(P, ST_GIVEUP, 1);
-    stat_add(P, ST_FRAMES, L.cnt);
-    if (stats_on(P)) stat_add(P, ST_T_MAIN, __builtin_amdgcn_s_memtime() - t1);
-  }
+  *P.cout = c;
 }
 
-// The next run after r with an entry (lane 0; every prologue is published by
-// now), or nruns.
-XYWS_DEV uint64_t next_visible(const run_params& P, uint64_t r) {
-  for (uint64_t j = r + 1; j < P.nruns; j++)
-    if (st_load(P.rec + j * R_WORDS + R_H) != NONE) return j;
-  return P.nruns;
-}
-
-// The piece of run r as its workgroup recorded it (lane 0). Its hand-over is
-// good only if its record is this call's and its successor's published entry
-// is the one its chain landed on.
-XYWS_DEV void load_piece(const run_params& P, walk_t& w, uint64_t r) {
-  const uint64_t* rec = P.rec + r * R_WORDS;
-  const uint64_t okw = st_load(rec + R_OK);
-  w.r = r;
-  w.efrom = st_load(rec + R_H);
-  w.ecarry = r == 0 ? 1u : 0u;
-  w.cnt = st_load(rec + R_CNT);
-  w.tail = st_load(rec + R_TAIL);
-  w.first = st_load(rec + R_FIRST);
-  w.F = get_state(rec + R_F0);
-  w.wlim = st_load(rec + R_WN);
-  w.succ = okw >> 32;
-  w.tmo = (okw & TMO_BIT) ? 1u : 0u;
-  w.ok = (okw & OK_BIT) ? 1u : 0u;
-  if (w.ok && w.succ < P.nruns && st_load(rec + R_HN) != st_load(P.rec + w.succ * R_WORDS + R_H)) w.ok = 0;
-}
-
-// Set up a chase from state S with the given successor limits (lane 0).
+// Fast finish of the call, by the run that finished last (whole workgroup):
+// every run's record was written with sc1 stores before its done-count add,
+// and is read here with sc1 loads after this run's add returned last
+// (MI355X_MICROARCH.md, hand-off table row 1). When every run with an entry
+// landed exactly on its successor's published entry (the usual case): frame
+// counts, descriptor ordinals and the final state by a block-wide scan over
+// the run records, and the call's outputs. Otherwise the repair flag is set
+// and k_stream_finish walks the runs (it reads the batch bytes other runs
+// wrote, which needs the kernel boundary).
 template <class G>
-XYWS_DEV void chain_start(lds_t<G>& L, const cstate& S, uint64_t hn, uint64_t Wn, uint64_t succ) {
-  L.S = S;
-  L.S.st &= ~S_CUT;
-  L.hn = hn; L.Wn = Wn; L.succ = succ;
-  L.known = 1; L.cnt = 0; L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.dense = 0; L.tmo = 0;
-  L.first_after = NONE;
-  L.best = 0;
-}
-
-// Walk the runs from run 0 along their successors, repairing every boundary
-// whose chain did not land on the successor's entry, then the frame count, the
-// carry and the descriptor plan (one workgroup; every run has exited).
-template <class G>
-__global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
-  lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
-  const uint32_t tid = threadIdx.x;
-  seg_io<G> io;
-  const uint64_t E = st_load(reinterpret_cast<const uint64_t*>(P.head + HEAD_EPOCH)) + 1;
+XYWS_DEV void finish_fast(const run_params& P, lds_t<G>& L, uint32_t tid) {
+  const uint64_t E = L.E;
   // Fast path (every run with an entry landed exactly on its successor's
   // entry: the usual case): frame counts, descriptor ordinals and the final
   // state by a block-wide scan over the run records, no serial walk. A run is
@@ -1642,6 +1586,169 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
     if (tid == 0) L.act = any_bad ? 1u : 0u;
     __syncthreads();
   }
+  if (tid == 0) {
+    if (L.act) {
+      __hip_atomic_store(P.head + HEAD_REPAIR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      xyws_carry cin;
+      for (int i = 0; i < 8; i++)
+        reinterpret_cast<uint64_t*>(&cin)[i] = st_load(reinterpret_cast<const uint64_t*>(P.cin) + i);
+      write_outputs(P, cin, L.aux2, L.S);
+    }
+  }
+}
+
+// End of a run (every workgroup, whatever its path): the records it wrote
+// (lane 0, sc1) have landed, then one done-count add; the run whose add comes
+// last finishes the call.
+template <class G>
+XYWS_DEV void end_of_run(const run_params& P, lds_t<G>& L, uint32_t tid) {
+  if (tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    L.ticket = atomicAdd(P.head + HEAD_DONE, 1u) + 1 == P.nruns ? 1u : 0u;
+  }
+  __syncthreads();
+  if (L.ticket) finish_fast<G>(P, L, tid);
+}
+
+// ---------------------------------------------------------------- kernels
+template <class G>
+__global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
+  lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) {
+    L.ticket = atomicAdd(P.head, 1u);
+    L.E = st_load(reinterpret_cast<const uint64_t*>(P.head + HEAD_EPOCH)) + 1;
+  }
+  __syncthreads();
+  const uint32_t run = uniform32(L.ticket);
+  if (run >= P.nruns) return;
+  uint64_t* rec = P.rec + (uint64_t)run * R_WORDS;
+  if (tid == 0) st_store(rec + R_ECNT, 0);  // no descriptors unless k_stream_finish plans them
+  const uint64_t rng_end = run + 1 < P.nruns ? (uint64_t)(run + 1) * P.rbytes : NONE;
+  seg_io<G> io;
+  uint64_t wlo, ss0;
+  bool in_lds = false;
+  if (run == 0) {
+    if (tid == 0) {
+      // snapshot of the incoming carry for k_stream_finish / k_stream_emit
+      // (the caller's carry may alias the carry out, which finish writes)
+      xyws_carry cz;
+      if (P.cin_user) {
+        cz = *P.cin_user;
+      } else {
+        for (int i = 0; i < 64; i++) reinterpret_cast<uint8_t*>(&cz)[i] = 0;
+      }
+      // (sc1 stores: the call's finishing run reads them, on any CU)
+      for (int i = 0; i < 8; i++)
+        st_store(reinterpret_cast<uint64_t*>(P.cin) + i, reinterpret_cast<const uint64_t*>(&cz)[i]);
+      uint64_t c0;
+      L.S = initial_state(P, &cz, c0);
+      L.cnt = c0;
+      st_store(rec + R_H, P.lo);
+      st_store(rec + R_W, P.lo);
+      put_state(rec + R_S0, L.S);
+      st_store(rec + R_HEAD, c0);
+    }
+    wlo = P.lo;
+    ss0 = 0;
+  } else {
+    // claim the own prologue (a predecessor that finds it unclaimed gives up
+    // on this run instead of waiting for a workgroup that may not be running)
+    if (tid == 0) granule_store(P.flags + 2 * (uint64_t)run, flag_claimed(L.E), 0);
+    prologue<G>(P, L, io, tid, run);
+    if (L.aux2 == NONE) {  // no entry: the chain of an earlier run covers this range
+      end_of_run<G>(P, L, tid);
+      return;
+    }
+    wlo = uniform64(L.aux2);
+    // the chain starts in the scanned segment (usual) or on the grid after it
+    const uint64_t a1 = uniform64(L.aux1);
+    ss0 = a1 + (wlo - a1) / G::SEG * G::SEG;
+    in_lds = ss0 == a1;
+    // (the next segment's loads were issued before the scan)
+    if (in_lds && ss0 + G::SEG < P.hi && io.pf != ss0 + G::SEG) io.issue(P, ss0 + G::SEG, tid);
+  }
+  if (tid == 0) {
+    L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.tmo = 0; L.first_after = NONE;
+    if (run == 0) L.dense = 0;
+    L.known = rng_end == NONE;
+    L.hn = NONE; L.Wn = NONE; L.succ = P.nruns; L.scan_j = run + 1;
+  }
+  __syncthreads();
+  uint64_t t1 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
+  run_chain(P, L, io, tid, ss0, in_lds, wlo, rng_end, run);
+  if (tid == 0) {
+    uint64_t* rec = P.rec + (uint64_t)run * R_WORDS;
+    const bool ok = !L.tmo && (L.succ >= P.nruns || (L.past && L.ok));
+    st_store(rec + R_OK, (ok ? OK_BIT : 0) | (L.tmo ? TMO_BIT : 0) | ((uint64_t)L.succ << 32));
+    st_store(rec + R_HN, L.hn);
+    st_store(rec + R_WN, L.Wn);
+    st_store(rec + R_CNT, L.cnt);
+    st_store(rec + R_TAIL, L.tail);
+    st_store(rec + R_FIRST, L.first_after);
+    put_state(rec + R_F0, L.S);
+    st_store(rec + R_EP, L.E);
+    if (!ok) stat_add(P, ST_BAD, 1);
+    if (L.tmo) stat_add(P, ST_GIVEUP, 1);
+    stat_add(P, ST_FRAMES, L.cnt);
+    if (stats_on(P)) stat_add(P, ST_T_MAIN, __builtin_amdgcn_s_memtime() - t1);
+  }
+  end_of_run<G>(P, L, tid);
+}
+
+// The next run after r with an entry (lane 0; every prologue is published by
+// now), or nruns.
+XYWS_DEV uint64_t next_visible(const run_params& P, uint64_t r) {
+  for (uint64_t j = r + 1; j < P.nruns; j++)
+    if (st_load(P.rec + j * R_WORDS + R_H) != NONE) return j;
+  return P.nruns;
+}
+
+// The piece of run r as its workgroup recorded it (lane 0). Its hand-over is
+// good only if its record is this call's and its successor's published entry
+// is the one its chain landed on.
+XYWS_DEV void load_piece(const run_params& P, walk_t& w, uint64_t r) {
+  const uint64_t* rec = P.rec + r * R_WORDS;
+  const uint64_t okw = st_load(rec + R_OK);
+  w.r = r;
+  w.efrom = st_load(rec + R_H);
+  w.ecarry = r == 0 ? 1u : 0u;
+  w.cnt = st_load(rec + R_CNT);
+  w.tail = st_load(rec + R_TAIL);
+  w.first = st_load(rec + R_FIRST);
+  w.F = get_state(rec + R_F0);
+  w.wlim = st_load(rec + R_WN);
+  w.succ = okw >> 32;
+  w.tmo = (okw & TMO_BIT) ? 1u : 0u;
+  w.ok = (okw & OK_BIT) ? 1u : 0u;
+  if (w.ok && w.succ < P.nruns && st_load(rec + R_HN) != st_load(P.rec + w.succ * R_WORDS + R_H)) w.ok = 0;
+}
+
+// Set up a chase from state S with the given successor limits (lane 0).
+template <class G>
+XYWS_DEV void chain_start(lds_t<G>& L, const cstate& S, uint64_t hn, uint64_t Wn, uint64_t succ) {
+  L.S = S;
+  L.S.st &= ~S_CUT;
+  L.hn = hn; L.Wn = Wn; L.succ = succ;
+  L.known = 1; L.cnt = 0; L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.dense = 0; L.tmo = 0;
+  L.first_after = NONE;
+  L.best = 0;
+}
+
+// Walk the runs from run 0 along their successors, repairing every boundary
+// whose chain did not land on the successor's entry, then the frame count, the
+// carry and the descriptor plan (one workgroup; every run has exited).
+template <class G>
+__global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
+  lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
+  const uint32_t tid = threadIdx.x;
+  seg_io<G> io;
+  const uint64_t E = st_load(reinterpret_cast<const uint64_t*>(P.head + HEAD_EPOCH)) + 1;
+  if (tid == 0) L.act = __hip_atomic_load(P.head + HEAD_REPAIR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
   if (L.act) {
   // Serial walk with repairs. Lane 0 keeps the current chain piece in L.wk:
   // the run whose descriptor plan it fills (r, efrom, ecarry), its frames
@@ -1752,45 +1859,19 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
     __syncthreads();
   }
   }  // serial walk with repairs
-  // every run has exited: the ticket starts the next call at zero; the epoch
-  // word advances (the prologue flags of this call read as stale from now on)
+  if (L.act && tid == 0) {
+    xyws_carry cin;
+    for (int i = 0; i < 8; i++) reinterpret_cast<uint64_t*>(&cin)[i] = st_load(reinterpret_cast<const uint64_t*>(P.cin) + i);
+    write_outputs(P, cin, L.aux2, L.S);
+  }
+  // every run has exited: the ticket and the done count start the next call
+  // at zero; the epoch word advances (this call's entry granules read as stale
+  // from now on)
   if (tid == 0) {
     P.head[0] = 0;
+    P.head[HEAD_DONE] = 0;
+    P.head[HEAD_REPAIR] = 0;
     st_store(reinterpret_cast<uint64_t*>(P.head + HEAD_EPOCH), E);
-    const uint64_t total = L.aux2;
-    const cstate o = L.S;
-    if (P.nframes) *P.nframes = total;
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(P.head + 2), total, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    if (P.cout) {
-      const uint64_t lo = P.lo, hi = P.hi;
-      xyws_carry c;
-      for (int i = 0; i < 64; i++) reinterpret_cast<uint8_t*>(&c)[i] = 0;
-      c.frames_total = P.cin->frames_total + total;
-      if (o.st & S_PARTIAL) {
-        uint32_t nb = 0;
-        if (o.st & S_PARTCARRY) {
-          for (; nb < P.cin->hdr_len; nb++) c.hdr[nb] = P.cin->hdr[nb];
-          for (uint64_t q = lo; q < hi && nb < 14; q++) c.hdr[nb++] = P.base[q];
-        } else {
-          for (uint64_t q = o.X; q < hi && nb < 14; q++) c.hdr[nb++] = P.base[q];
-        }
-        c.hdr_len = (uint8_t)nb;
-      } else if (o.X > hi && !(o.st & S_NOCOV)) {
-        if (o.st & S_CARRIED) {
-          c.payload_remaining = P.cin->payload_remaining - (hi - lo);
-          c.phase = P.cin->phase + (hi - lo);
-          for (int i = 0; i < 4; i++) c.key[i] = P.cin->key[i];
-        } else {
-          const hdr_info hh = (o.st & S_HDRCARRY) ? header_carried(P, P.cin) : hdr_global(P, o.cov_start, NONE);
-          c.payload_remaining = hh.plen - (hi - o.cov_ps);
-          c.phase = hi - o.cov_ps;
-          c.key[0] = (uint8_t)hh.key; c.key[1] = (uint8_t)(hh.key >> 8);
-          c.key[2] = (uint8_t)(hh.key >> 16); c.key[3] = (uint8_t)(hh.key >> 24);
-        }
-      }
-      *P.cout = c;
-    }
   }
 }
 
@@ -1906,7 +1987,7 @@ void stream_scratch_free(stream_scratch* s) {
   s->max_runs = 0;
 }
 
-static uint64_t flags_bytes(uint64_t n) { return (8 * n + 255) & ~255ull; }
+static uint64_t flags_bytes(uint64_t n) { return (16 * n + 255) & ~255ull; }
 
 static int scratch_grow(stream_scratch* s, uint64_t runs) {
   if (s->mem && runs <= s->max_runs) return XYWS_OK;
