@@ -381,7 +381,8 @@ def main():
                  "cyc_scan_check", "cyc_scan_resolve", "cyc_dense_entry", "cyc_dense_chase", "cyc_prologue", "cyc_main", "cyc_wait",
                  "cyc_fill", "cyc_chase_sync", "cyc_xor", "cyc_tail", "cyc_prefetch_issue", "cyc_chase_pass",
                  "cyc_pro_fill", "cyc_pro_scan", "cyc_pro_publish", "dense_no_entry", "dense_chase_fail",
-                 "dense_mismatch", "dense_overflow", "giveups", "bridges"]
+                 "dense_mismatch", "dense_overflow", "giveups", "bridges", "steal_requests", "steals",
+                 "stolen_segments"]
         for _ in range(2):
             dec.opts |= _lib.OPT_STATS
             dec.decode(bufs[0], cap=0, count=False, carry=False)

@@ -18,9 +18,16 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 OPT_TEST_GIVEUP = 0x100000  # xyws_stream.h: odd runs give up on their successor (finish bridges them)
+OPT_STEAL = 0x400000        # work stealing (off by default)
+OPT_TEST_STEAL = 0x800000   # every fourth run starts late; pieces of 1 segment and up are taken
 MODES = {"fused": {}, "serial": {"serial": True}, "runs1k": {"small_segments": True},
          "giveup": {"opts": OPT_TEST_GIVEUP},
-         "runs1k_giveup": {"small_segments": True, "opts": OPT_TEST_GIVEUP}}
+         "runs1k_giveup": {"small_segments": True, "opts": OPT_TEST_GIVEUP},
+         "steal_prod": {"opts": OPT_STEAL},
+         "steal": {"opts": OPT_TEST_STEAL},
+         "runs1k_steal": {"small_segments": True, "opts": OPT_TEST_STEAL},
+         "steal_giveup": {"opts": OPT_TEST_STEAL | OPT_TEST_GIVEUP},
+         "runs1k_steal_giveup": {"small_segments": True, "opts": OPT_TEST_STEAL | OPT_TEST_GIVEUP}}
 
 
 @pytest.fixture(scope="module")
@@ -137,7 +144,7 @@ def test_stream_split_with_carry(ws, name, mode):
         assert [[x[0] + k, x[1] + k] + x[2:] for x in fb] == g["frames"][s["n1"]:]
 
 
-@pytest.mark.parametrize("mode", ["fused", "runs1k", "runs1k_giveup"])
+@pytest.mark.parametrize("mode", ["fused", "runs1k", "runs1k_giveup", "runs1k_steal", "runs1k_steal_giveup"])
 def test_fuzz_random_streams_vs_oracle(ws, oracle, mode):
     """Random frame soups + random cut points, GPU vs oracle."""
     rng = streams.SplitMix(0xF022)
@@ -277,7 +284,12 @@ CONFIG_CASES = ([(n, "fused") for n in [
     "c4_mixed", "c5_shard0", "c5_shard7"]] +
     [(n, "runs1k") for n in ["t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m"]] +
     [(n, "giveup") for n in ["t_mixed_8m", "c1_text_4k", "c2_bin_256", "c4_mixed", "c5_shard3"]] +
-    [(n, "runs1k_giveup") for n in ["t_bin_256_x4096", "t_mixed_8m"]])
+    [(n, "runs1k_giveup") for n in ["t_bin_256_x4096", "t_mixed_8m"]] +
+    [(n, "steal_prod") for n in ["c3_bin_64k", "c4_mixed"]] +
+    [(n, "steal") for n in ["t_mixed_8m", "c1_text_4k", "c2_bin_256", "c3_bin_64k", "c4_mixed", "c5_shard2"]] +
+    [(n, "runs1k_steal") for n in ["t_bin_256_x4096", "t_mixed_8m", "t_bin_64k_x64"]] +
+    [(n, "steal_giveup") for n in ["t_mixed_8m", "c2_bin_256", "c4_mixed"]] +
+    [(n, "runs1k_steal_giveup") for n in ["t_mixed_8m"]])
 
 
 def frames_digest(oracle, r, n):
@@ -344,3 +356,27 @@ def test_device_error_word_reads_zero_after_clean_decodes(ws):
     dec.decode(view, cap=8)
     assert dec.ctx.last_device_error() == 0
     assert dec.ctx.last_device_error() == 0
+
+
+@pytest.mark.parametrize("name,small", [("c3_bin_64k", False), ("c4_mixed", False), ("t_mixed_8m", True)])
+def test_work_stealing_takes_pieces(ws, oracle, name, small):
+    """With late-starting runs (test mode) the runs that finish first take the
+    tails of the late runs' ranges: the stats must show accepted splits, and
+    bytes, frames and carry must still be the reference's."""
+    from xynet_amd import _lib
+    buf, c = tools_batch(name)
+    dec = ws.frame_decoder(small_segments=small, opts=OPT_TEST_STEAL | _lib.OPT_STATS)
+    n = c["decoded_frames"]
+    r = dec.decode(buf, cap=n)
+    out = (C.c_uint64 * _lib.NSTATS)()
+    stream = torch.cuda.current_stream()
+    assert dec.ctx.L.xyws_debug_stats(dec.ctx.h, C.c_void_p(stream.cuda_stream), out) == 0
+    assert out[_lib.ST_STEAL_ACC] > 0, list(out)
+    assert out[_lib.ST_STEAL_SEGS] >= out[_lib.ST_STEAL_ACC]
+    assert r.nframes == n
+    assert dev_digest(buf) == c["out_digest"]
+    assert carry_list(dec.carry()) == c["carry"]
+    assert frames_digest(oracle, r, n) == c["frames_digest"]
+    assert dec.ctx.last_device_error() == 0
+    del buf, r
+    torch.cuda.empty_cache()

@@ -21,6 +21,10 @@ OPT_STATS = 0x100
 OPT_SMALL_SEG = 0x200
 OPT_WG512 = 0x40000
 OPT_TEST_GIVEUP = 0x100000
+OPT_STEAL = 0x400000
+OPT_TEST_STEAL = 0x800000
+# debug stats indices (xyws_stream.hip)
+ST_GIVEUP, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS = 32, 33, 34, 35, 36
 ERRORS = {-1: "invalid argument", -2: "HIP runtime error", -3: "device allocation failed",
           -4: "scratch capacity exceeded", -5: "device-side error"}
 

@@ -59,6 +59,12 @@
 
 namespace {
 
+
+#ifndef XYWS_EXP_FINISH
+#define XYWS_EXP_FINISH 0  // timing experiments (scripts/ab.sh variants): 1 = no repair walk, 2 = no fast path,
+                           // 3 = no descriptor plan stores, 4 = no outputs
+#endif
+
 constexpr uint64_t NONE = ~0ull;
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr uint32_t PAD = 32;          // LDS bytes after the segment (5-dword header reads)
@@ -78,6 +84,14 @@ constexpr uint32_t OOB = 0x80000000u; // buffer offset past every range: load 0,
 constexpr int AUX_NT = 2;             // buffer cache policy: nontemporal
 constexpr uint64_t PLEN_SPEC_MAX = 1ull << 46;
 constexpr uint32_t MAX_RUNS = 1024;
+// work stealing: a run is asked for its tail when it has at least this many
+// segments left after the current one; the piece is at least this long
+#ifndef XYWS_STEAL_MIN_LEFT
+#define XYWS_STEAL_MIN_LEFT 8
+#endif
+#ifndef XYWS_STEAL_MIN_PIECE
+#define XYWS_STEAL_MIN_PIECE 3
+#endif
 
 
 // chase-state bits
@@ -131,6 +145,8 @@ enum {
   R_F0 = 14,                                        // final state (5 words)
   R_EFROM = 20, R_ECNT, R_EORD, R_ECARRY,           // emission plan (k_stream_finish)
   R_EP = 24,                                        // epoch of the call that wrote the results
+  R_T0, R_T1, R_T2,                                 // stats mode: s_memrealtime at start, after the prologue, at the end
+  R_SPLIT,                                          // own runs: the split segment a thief took the rest from (NONE: none)
   R_WORDS = 32
 };
 // R_OK bits
@@ -155,8 +171,6 @@ XYWS_DEV uint64_t flag_published(uint64_t E) { return (E << 1) | 1u; }
 constexpr uint64_t G_NONE = (1ull << 46) - 1;
 XYWS_DEV uint64_t granule_tag(uint64_t E) { return (E & 0x1FFFull) << 51; }
 constexpr uint32_t HEAD_EPOCH = 4;   // u32 index of the u64 epoch word in head[]
-constexpr uint32_t HEAD_DONE = 6;    // u32: runs finished in this call (the last one finishes the call)
-constexpr uint32_t HEAD_REPAIR = 7;  // u32: the fast finish found a bad hand-off (k_stream_finish walks)
 
 XYWS_DEV void granule_store(uint64_t* g, uint64_t a, uint64_t b) {
   const u32x4 v = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
@@ -169,21 +183,47 @@ XYWS_DEV void granule_load(const uint64_t* g, uint64_t& a, uint64_t& b) {
   b = (uint64_t)v.z | ((uint64_t)v.w << 32);
 }
 
+// Work stealing. A run's range is cut at segment granularity when a workgroup
+// that finished early asks for it: the tail of the range becomes a PIECE that
+// the thief decodes like a run (its own entry scan, chain and record), placed
+// between the run and its successor. Records, entry granules and descriptor
+// plans are indexed by a flat index in batch order: run r = 2r, its piece =
+// 2r + 1 (at most one piece per run). Per run, a split word (16 bytes, the
+// first u64 used) holds (E << 24) | (state << 22) | e', e' the first segment
+// of the piece:
+//   FREE   set by the run when it starts (it can be asked),
+//   REQ    a thief asks (atomic CAS from FREE),
+//   ACC    the run agrees, the piece starts at segment e',
+//   CLS    the run will not split (no entry, too little left, successor
+//          already looked up, or a refused request).
+// The run reads its split word with one LDS-DMA load per segment (issued
+// before the prefetch, so the fill's wait covers it: no stall, no register).
+enum { SP_FREE = 0, SP_REQ = 1, SP_ACC = 2, SP_CLS = 3 };
+XYWS_DEV uint64_t split_word(uint64_t E, uint32_t state, uint32_t e) {
+  return (E << 24) | ((uint64_t)state << 22) | (e & 0x3FFFFFu);
+}
+XYWS_DEV uint32_t split_state(uint64_t w) { return (uint32_t)(w >> 22) & 3u; }
+XYWS_DEV uint32_t split_seg(uint64_t w) { return (uint32_t)w & 0x3FFFFFu; }
+XYWS_DEV bool split_is(uint64_t w, uint64_t E, uint32_t state) { return (w >> 24) == (E & ((1ull << 40) - 1)) && split_state(w) == state; }
+
 struct run_params {
   uint8_t* base;
   uint64_t lo, hi;
   uint64_t rbytes;        // bytes per run range (multiple of 16); run r: [r*rbytes, (r+1)*rbytes)
   uint32_t nruns;
+  uint32_t nflat;         // 2 * nruns: records / granules / plans (run r = 2r, its piece = 2r + 1)
+  uint64_t* split;        // per run: split word (2 x u64)
+  uint64_t* prog;         // per run: (E << 24) | segment being decoded (thieves pick the run with most left)
   const xyws_carry* cin_user;  // caller's incoming carry (nullable; may alias cout)
   xyws_carry* cin;        // private snapshot of it, written by run 0 (finish/emit read it)
   xyws_carry* cout;
   xyws_frame* frames;
   uint64_t cap;
   uint64_t* nframes;
-  uint64_t* rec;          // R_WORDS per run
-  uint64_t* flags;        // per run: entry granule (2 x u64, see flag_claimed)
-  uint32_t* head;         // [0] ticket, [1] error word, [2..3] u64 total, [4..5] u64 epoch, [6] done,
-                          // [7] repair; [16..32) carry snapshot; stats at [32..)
+  uint64_t* rec;          // R_WORDS per flat index
+  uint64_t* flags;        // per flat index: entry granule (2 x u64, see flag_claimed)
+  uint32_t* head;         // [0] ticket, [1] error word, [2..3] u64 total, [4..5] u64 epoch;
+                          // [16..32) carry snapshot; stats at [32..)
   uint32_t opts;
 };
 
@@ -201,7 +241,15 @@ struct __attribute__((aligned(16))) lds_t {
   cstate B;  // k_stream_finish: exact state handed to a repaired run
   uint64_t hn, Wn, succ, first_after, cnt, tail, aux0, aux1, aux2, bcnt, bfirst;
   uint64_t E;      // this call's epoch
-  uint64_t scan_j; // successor lookup: next run to examine
+  xyws_carry cinc; // k_stream_finish: the incoming-carry snapshot
+  uint64_t scan_j; // successor lookup: next flat index to examine
+  uint64_t ib, ie;     // the item (own run or piece) the workgroup decodes next: its byte range
+  uint64_t rng_end;    // end of the current run's range (a run's shrinks when a thief takes its tail)
+  uint64_t rs;         // start of the current run's range (segment grid of the split word)
+  uint64_t split_e;    // own run: first segment of the piece taken from it (NONE: none)
+  uint64_t split_poll[2] __attribute__((aligned(16)));  // LDS-DMA target: the run's split word
+  uint64_t self;       // flat index of the run or piece being decoded
+  uint32_t victim;     // 1: the current run answers steal requests (an own run, not yet closed)
   walk_t wk;       // k_stream_finish: the current chain piece
   uint32_t nfl, pass_hi, known, past, ok, done, end, best, ticket, act, repaired, ccnt, ucnt, keepn, ovf;
   uint32_t tmo;    // successor given up on (write limit = own range end, bridged by k_stream_finish)
@@ -228,7 +276,7 @@ enum { ST_RUNS = 0, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRA
        ST_P_WIN, ST_P_CAND, ST_P_UND, ST_P_TCOMP, ST_P_TCHECK, ST_P_TRES, ST_D_TENT, ST_D_TCHASE,
        ST_T_PRO = 16, ST_T_MAIN, ST_T_WAIT, ST_T_FILL, ST_T_CHASE, ST_T_XOR, ST_T_TAIL, ST_T_PF, ST_T_CP,
        ST_P_FILL, ST_P_SCAN, ST_P_PUB, ST_D_NOENT, ST_D_CHASE, ST_D_MISMATCH, ST_D_OVF,
-       ST_GIVEUP = 32, ST_BRIDGE };
+       ST_GIVEUP = 32, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS };
 XYWS_DEV void stat_add(const run_params& P, uint32_t i, uint64_t v) {
   if (stats_on(P)) atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + i, (unsigned long long)v);
 }
@@ -622,7 +670,11 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
 // does not fit the segment ends the pass (pass_hi) and the serial chase
 // continues it. Called only where no limit lies in the segment.
 template <class G>
-XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid, bool unm, bool past) {
+XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid_in, bool unm, bool past) {
+  // (the lane index made opaque here: its LDS address math is recomputed per
+  // pass instead of being hoisted out of the segment loop and spilled)
+  uint32_t tid = tid_in;
+  asm volatile("" : "+v"(tid));
   constexpr uint32_t NSB = G::NSB, SB = G::SB, SECT = G::SECT;
   constexpr uint32_t STOP = G::SEG - XYWS_MAX_FRAME_HEADER_SIZE + 1;  // headers wholly in LDS start below
   const uint32_t lane = tid & 63u, gl = lane & 15u, sb = (tid >> 6) * 4 + (lane >> 4);
@@ -869,29 +921,39 @@ XYWS_DEV bool wait_published(const run_params& P, uint32_t j, uint64_t E, uint64
   return true;
 }
 
-// The next run after `run` that has an entry (lane 0), starting the search at
-// L.scan_j. Returns LK_FOUND with (hn, Wn, succ) (succ = nruns: none), or
-// LK_GIVEUP with succ = the run whose entry is not published: its workgroup
-// has not started (not every workgroup of the grid is resident, e.g. beside a
-// concurrent decode, and waiting for one that is not could deadlock), or its
-// bounded wait timed out (reported in the error word). Never uses a granule
-// not published in this call. A run given up on is bridged by k_stream_finish.
+// The next run or piece after L.self that has an entry (lane 0), starting the
+// search at flat index L.scan_j. Returns LK_FOUND with (hn, Wn, succ) (succ =
+// nflat: none), or LK_GIVEUP with succ = the run whose entry is not published:
+// its workgroup has not started (not every workgroup of the grid is resident,
+// e.g. beside a concurrent decode, and waiting for one that is not could
+// deadlock), or its bounded wait timed out (reported in the error word). A
+// piece exists only when its run agreed to the split; its thief is running,
+// so it is waited for. Never uses a granule not published in this call. A
+// run given up on is bridged by k_stream_finish.
 enum { LK_FOUND = 0, LK_GIVEUP = 1 };
 template <class G>
-XYWS_DEV uint32_t lookup_successor(const run_params& P, lds_t<G>& L, uint64_t& hn, uint64_t& Wn, uint64_t& succ,
-                                   uint32_t run) {
-  const uint64_t E = L.E;
-  for (uint64_t j = L.scan_j; j < P.nruns; j++) {
+XYWS_DEV uint32_t lookup_successor(const run_params& P, lds_t<G>& L, uint64_t& hn, uint64_t& Wn, uint64_t& succ) {
+  const uint64_t E = L.E, self = L.self;
+  for (uint64_t j = L.scan_j; j < P.nflat; j++) {
     L.scan_j = j;
     uint64_t a, b;
-    granule_load(P.flags + 2 * j, a, b);
-    // (test mode: odd runs give up on their successor at once)
-    const bool test = (P.opts & XYWS_OPT_TEST_GIVEUP) && (run & 1u);
-    if (test || (a >> 1) < E || (a != flag_published(E) && !wait_published(P, (uint32_t)j, E, a, b)) ||
-        (b & (0x1FFFull << 51)) != granule_tag(E)) {
-      if (a == flag_published(E) && (b & (0x1FFFull << 51)) != granule_tag(E)) atomicOr(P.head + 1, 8u);
-      succ = j;
-      return LK_GIVEUP;
+    if (j & 1) {  // the piece of run j/2: only if that run agreed to the split
+      const bool own = j == self + 1 && !(self & 1);
+      if (own ? L.split_e == NONE : !split_is(st_load(P.split + 2 * (j >> 1)), E, SP_ACC)) continue;
+      if (!wait_published(P, (uint32_t)j, E, a, b) || (b & (0x1FFFull << 51)) != granule_tag(E)) {
+        succ = j;
+        return LK_GIVEUP;
+      }
+    } else {
+      granule_load(P.flags + 2 * j, a, b);
+      // (test mode: odd runs give up on their successor at once)
+      const bool test = (P.opts & XYWS_OPT_TEST_GIVEUP) && ((self >> 1) & 1u) && !(self & 1);
+      if (test || (a >> 1) < E || (a != flag_published(E) && !wait_published(P, (uint32_t)j, E, a, b)) ||
+          (b & (0x1FFFull << 51)) != granule_tag(E)) {
+        if (a == flag_published(E) && (b & (0x1FFFull << 51)) != granule_tag(E)) atomicOr(P.head + 1, 8u);
+        succ = j;
+        return LK_GIVEUP;
+      }
     }
     const uint64_t h = b & G_NONE;
     if (h != G_NONE) {
@@ -903,7 +965,7 @@ XYWS_DEV uint32_t lookup_successor(const run_params& P, lds_t<G>& L, uint64_t& h
   }
   hn = NONE;
   Wn = NONE;
-  succ = P.nruns;
+  succ = P.nflat;
   return LK_FOUND;
 }
 
@@ -919,14 +981,51 @@ XYWS_DEV void dummy_stores(const run_params& P, uint64_t ss) {
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rz, OOB, k * G::NT * 16u, AUX_NT);  // distinct: not merged
 }
 
-// Apply the chain in L.S (set by lane 0 together with L.known/hn/Wn/succ and
-// zeroed counters) from the segment at ss0: every byte in [wlo, write limit) is XORed
-// with the key of the frame covering it, the write limit being the successor's
-// W (looked up before the first segment at or past rng_end, unless known). The
-// chase stops at the successor's W; L.ok tells whether it landed on its entry.
+// A run that will not split any more (lane 0; it is about to look up its
+// successor, or it is done): close its split word, refusing a pending request.
+XYWS_DEV void close_split(const run_params& P, uint64_t* sw, uint64_t E) {
+  const unsigned long long fr = split_word(E, SP_FREE, 0);
+  const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long*>(sw), fr,
+                                           (unsigned long long)split_word(E, SP_CLS, 0));
+  if (old != fr && split_is(old, E, SP_REQ)) st_store(sw, split_word(E, SP_CLS, 0));
+}
+
+// A steal request seen in the split word the run DMA'd into LDS (lane 0, at
+// the top of the segment at ss, after the fill's wait covered that load): the
+// run keeps the current and the next segment and about half of the rest
+// (less one segment, the thief's entry scan), the thief gets the tail.
+template <class G>
+XYWS_DEV void answer_split(const run_params& P, lds_t<G>& L, uint64_t ss) {
+  const uint64_t w = L.split_poll[0];
+  if (!split_is(w, L.E, SP_REQ)) return;
+  uint64_t* sw = P.split + 2 * (L.self >> 1);
+  const uint64_t rend = L.rng_end < P.hi ? L.rng_end : P.hi;
+  const uint64_t i = (ss - L.rs) / G::SEG, nseg = (rend - L.rs + G::SEG - 1) / G::SEG;
+  const uint64_t m = nseg > i ? nseg - i : 0;
+  const uint64_t e = i + 2 + (m > 3 ? (m - 3) / 2 : 0);
+  const uint64_t minp = (P.opts & XYWS_OPT_TEST_STEAL) ? 1 : XYWS_STEAL_MIN_PIECE;
+  if (!L.known && e + minp <= nseg && e < (1u << 22)) {
+    L.split_e = e;
+    L.rng_end = L.rs + e * G::SEG;
+    st_store(sw, split_word(L.E, SP_ACC, (uint32_t)e));
+    stat_add(P, ST_STEAL_ACC, 1);
+    stat_add(P, ST_STEAL_SEGS, nseg - e);
+  } else {
+    st_store(sw, split_word(L.E, SP_CLS, 0));
+  }
+  L.victim = 0;  // one answer per run
+}
+
+// Apply the chain in L.S (set by lane 0 together with L.known/hn/Wn/succ,
+// L.rng_end and zeroed counters) from the segment at ss0: every byte in [wlo,
+// write limit) is XORed with the key of the frame covering it, the write limit
+// being the successor's W (looked up before the first segment at or past
+// L.rng_end, unless known). The chase stops at the successor's W; L.ok tells
+// whether it landed on its entry. A run (L.victim) answers steal requests on
+// the way: its range end shrinks to the split.
 template <class G>
 XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint64_t ss0,
-                        bool in_lds, uint64_t wlo, uint64_t rng_end, uint32_t run) {
+                        bool in_lds, uint64_t wlo) {
   const bool stores = (P.opts & XYWS_OPT_PARSE_ONLY) == 0;
   const uint64_t wl = wlo > P.lo ? wlo : P.lo;
   // Pipeline: the registers of `io` always hold the loads of the segment the
@@ -950,15 +1049,19 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
   } while (0)
   // Once the next segment lies past the run's range the write limit is the
   // successor's W (its prologue published it long ago): looked up before the
-  // next segment's prefetch is decided.
+  // next segment's prefetch is decided. No split is agreed after that.
   auto lookup = [&](uint64_t nxt) {
-    if (tid == 0 && !L.known && nxt >= rng_end) {
+    if (tid == 0 && !L.known && nxt >= L.rng_end) {
       const uint64_t t0 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
-      uint64_t hn = NONE, Wn = NONE, succ = P.nruns;
-      if (lookup_successor(P, L, hn, Wn, succ, run) == LK_GIVEUP) {
+      if (L.victim) {
+        close_split(P, P.split + 2 * (L.self >> 1), L.E);
+        L.victim = 0;
+      }
+      uint64_t hn = NONE, Wn = NONE, succ = P.nflat;
+      if (lookup_successor(P, L, hn, Wn, succ) == LK_GIVEUP) {
         // unknown successor: write up to the own range end only and leave
         // the rest to k_stream_finish (never a stale record)
-        L.hn = NONE; L.Wn = rng_end; L.succ = succ; L.known = 1; L.tmo = 1;
+        L.hn = NONE; L.Wn = L.rng_end; L.succ = succ; L.known = 1; L.tmo = 1;
       } else {
         L.hn = hn; L.Wn = Wn; L.succ = succ; L.known = 1;
       }
@@ -970,19 +1073,33 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
     const uint64_t nx = ss + G::SEG;
     __syncthreads();  // the previous segment's LDS reads are done; L control words visible
     XYWS_STAMP(acc_tail);
-    const bool known = L.known != 0;
-    const uint64_t wlim = known ? L.Wn : rng_end;
-    const uint64_t whi = wlim < P.hi ? wlim : P.hi;
-    const bool fin0 = (L.end || L.done) && nx >= whi;
-    const bool pf = nx < P.hi && nx < wlim && !fin0 && io.pf != nx;
-    if (!(in_lds && ss == ss0)) {
+    const bool filled = !(in_lds && ss == ss0);
+    if (filled) {
 #pragma unroll
       for (uint32_t k = 0; k < G::CH; k++)
         *reinterpret_cast<u32x4*>(&L.seg[(k * G::NT + tid) * 16u]) = io.e[k];
       io.pf = NONE;
+      // (wave 0's fill waited for its loads, among them lane 0's split-word
+      // DMA, issued before them; the prefetch registers are free here: the
+      // lane-0 work of a run that can be split goes where they are dead)
+      asm volatile("" ::: "memory");
+      if (tid == 0 && L.victim) answer_split<G>(P, L, ss);
     }
     __syncthreads();
     XYWS_STAMP(acc_fill);
+    const bool known = L.known != 0;
+    const uint64_t wlim = known ? L.Wn : L.rng_end;
+    const uint64_t whi = wlim < P.hi ? wlim : P.hi;
+    const bool fin0 = (L.end || L.done) && nx >= whi;
+    const bool pf = nx < P.hi && nx < wlim && !fin0 && io.pf != nx;
+    if (tid == 0 && L.victim && filled) {
+      // progress for thieves, and the split word into LDS for the next
+      // iteration (both before the prefetch: the next fill's wait covers them)
+      const uint32_t r = (uint32_t)(L.self >> 1);
+      st_store(P.prog + r, (L.E << 24) | ((ss - L.rs) / G::SEG));
+      __builtin_amdgcn_global_load_lds((const void*)(P.split + 2 * r),
+                                       (__attribute__((address_space(3))) void*)L.split_poll, 16, 0, 16);
+    }
     // (issuing each chunk's next load right after its LDS write made hipcc wait
     // for the new loads inside the fill: the prefetch goes after the barrier)
     if (pf) io.issue(P, nx, tid, known ? wlim : NONE);
@@ -1362,10 +1479,9 @@ XYWS_DEV void scan_segment(const run_params& P, lds_t<G>& L, uint64_t ss, uint32
 }
 
 template <class G>
-XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint32_t run) {
+XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint64_t rb,
+                         uint64_t re) {
   const bool unm = (P.opts & XYWS_OPT_UNMASKED_HINT) != 0;
-  const uint64_t rb = (uint64_t)run * P.rbytes;
-  uint64_t re = rb + P.rbytes;
   if (re > P.hi) re = P.hi;
   if (tid == 0) L.aux0 = NONE;
   uint64_t tp = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
@@ -1398,17 +1514,18 @@ XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32
   __syncthreads();
 }
 
-// Prologue of run `run` (whole workgroup): the entry scan of its range, then
-// lane 0 publishes (h, W, entry state, head frames) in its record and sets its
-// flag to published for this call. The chain state is left in L, the scanned
-// segment in LDS (L.aux1), L.aux2 = W or NONE.
+// Prologue of the run or piece at flat index `self` (whole workgroup): the
+// entry scan of its range [rb, re), then lane 0 publishes (h, W, entry state,
+// head frames) in its record and its entry granule. The chain state is left
+// in L, the scanned segment in LDS (L.aux1), L.aux2 = W or NONE.
 template <class G>
-XYWS_DEV void prologue(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint32_t run) {
+XYWS_DEV void prologue(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint64_t self, uint64_t rb,
+                       uint64_t re) {
   const uint64_t t0 = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
-  find_entry(P, L, io, tid, run);
+  find_entry(P, L, io, tid, rb, re);
   const uint64_t tpub = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
   if (tid == 0) {
-    const uint64_t rng_end = run + 1 < P.nruns ? (uint64_t)(run + 1) * P.rbytes : NONE;
+    const uint64_t rng_end = re < P.hi ? re : NONE;
     const uint64_t q = L.aux0, ss = L.aux1;
     uint64_t h = NONE, W = NONE, hc = 0;
     cstate S;
@@ -1432,12 +1549,12 @@ XYWS_DEV void prologue(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t
         }
       }
     }
-    uint64_t* rec = P.rec + (uint64_t)run * R_WORDS;
+    uint64_t* rec = P.rec + self * R_WORDS;
     st_store(rec + R_H, h);
     st_store(rec + R_W, W);
     put_state(rec + R_S0, S);
     st_store(rec + R_HEAD, hc);
-    granule_store(P.flags + 2 * (uint64_t)run, flag_published(L.E),
+    granule_store(P.flags + 2 * self, flag_published(L.E),
                   (h == NONE ? G_NONE : (h | ((W - h) << 46))) | granule_tag(L.E));
     L.S = S;
     L.cnt = hc;
@@ -1453,235 +1570,215 @@ XYWS_DEV void prologue(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t
 }
 
 // The call's outputs (lane 0): frame count, total, carry out. cin: the
-// incoming-carry snapshot, o: the final chain state.
-XYWS_DEV void write_outputs(const run_params& P, const xyws_carry& cin, uint64_t total, const cstate& o) {
+// incoming-carry snapshot (in LDS), o: the final chain state. The carry is
+// assembled in 64-bit words (no byte array: nothing goes to scratch).
+XYWS_DEV void write_outputs(const run_params& P, const xyws_carry* cin, uint64_t total, const cstate& o) {
   if (P.nframes) *P.nframes = total;
   __hip_atomic_store(reinterpret_cast<uint64_t*>(P.head + 2), total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (!P.cout) return;
   const uint64_t lo = P.lo, hi = P.hi;
-  xyws_carry c;
-  for (int i = 0; i < 64; i++) reinterpret_cast<uint8_t*>(&c)[i] = 0;
-  c.frames_total = cin.frames_total + total;
+  uint64_t pr = 0, ph = 0, key = 0, hl = 0, h0 = 0, h1 = 0;  // h0/h1: header bytes 0..7 / 8..13
   if (o.st & S_PARTIAL) {
-    uint32_t nb = 0;
-    if (o.st & S_PARTCARRY) {
-      for (; nb < cin.hdr_len; nb++) c.hdr[nb] = cin.hdr[nb];
-      for (uint64_t q = lo; q < hi && nb < 14; q++) c.hdr[nb++] = P.base[q];
-    } else {
-      for (uint64_t q = o.X; q < hi && nb < 14; q++) c.hdr[nb++] = P.base[q];
+    // the incomplete header: carried bytes (if still incomplete) + the batch tail
+    const uint32_t c0 = (o.st & S_PARTCARRY) ? cin->hdr_len : 0u;
+    const uint64_t from = (o.st & S_PARTCARRY) ? lo : o.X;
+#pragma unroll
+    for (uint32_t i = 0; i < XYWS_MAX_FRAME_HEADER_SIZE; i++) {
+      uint64_t b = 0;
+      bool have = true;
+      if (i < c0) b = cin->hdr[i];
+      else if (from + (i - c0) < hi) b = P.base[from + (i - c0)];
+      else have = false;
+      if (have && hl == i) {
+        if (i < 8) h0 |= b << (8 * i); else h1 |= b << (8 * (i - 8));
+        hl++;
+      }
     }
-    c.hdr_len = (uint8_t)nb;
   } else if (o.X > hi && !(o.st & S_NOCOV)) {
     if (o.st & S_CARRIED) {
-      c.payload_remaining = cin.payload_remaining - (hi - lo);
-      c.phase = cin.phase + (hi - lo);
-      for (int i = 0; i < 4; i++) c.key[i] = cin.key[i];
+      pr = cin->payload_remaining - (hi - lo);
+      ph = cin->phase + (hi - lo);
+      key = (uint64_t)cin->key[0] | ((uint64_t)cin->key[1] << 8) | ((uint64_t)cin->key[2] << 16) |
+            ((uint64_t)cin->key[3] << 24);
     } else {
-      const hdr_info hh = (o.st & S_HDRCARRY) ? header_carried(P, &cin) : hdr_global(P, o.cov_start, NONE);
-      c.payload_remaining = hh.plen - (hi - o.cov_ps);
-      c.phase = hi - o.cov_ps;
-      c.key[0] = (uint8_t)hh.key; c.key[1] = (uint8_t)(hh.key >> 8);
-      c.key[2] = (uint8_t)(hh.key >> 16); c.key[3] = (uint8_t)(hh.key >> 24);
+      const hdr_info hh = (o.st & S_HDRCARRY) ? header_carried(P, cin) : hdr_global(P, o.cov_start, NONE);
+      pr = hh.plen - (hi - o.cov_ps);
+      ph = hi - o.cov_ps;
+      key = hh.key;
     }
   }
-  *P.cout = c;
+  // xyws_carry: payload_remaining, phase, frames_total, key[4] @24, hdr_len @28, hdr[14] @29
+  uint64_t* c = reinterpret_cast<uint64_t*>(P.cout);
+  c[0] = pr;
+  c[1] = ph;
+  c[2] = cin->frames_total + total;
+  c[3] = key | (hl << 32) | (h0 << 40);
+  c[4] = (h0 >> 24) | (h1 << 40);
+  c[5] = h1 >> 24;
+  c[6] = 0;
+  c[7] = 0;
 }
 
-// Fast finish of the call, by the run that finished last (whole workgroup):
-// every run's record was written with sc1 stores before its done-count add,
-// and is read here with sc1 loads after this run's add returned last
-// (MI355X_MICROARCH.md, hand-off table row 1). When every run with an entry
-// landed exactly on its successor's published entry (the usual case): frame
-// counts, descriptor ordinals and the final state by a block-wide scan over
-// the run records, and the call's outputs. Otherwise the repair flag is set
-// and k_stream_finish walks the runs (it reads the batch bytes other runs
-// wrote, which needs the kernel boundary).
+// k_stream_finish's fast path (whole workgroup; every run has exited). When
+// every run with an entry landed exactly on its successor's published entry
+// (the usual case): frame counts, descriptor ordinals and the final state by a
+// block-wide scan over the run records, no serial walk; L.act = 0, L.aux2 =
+// the frame total, L.S = the final state. A run is good when its record is
+// this call's, it did not give up on its successor, its chain landed on the
+// successor's entry and that entry is the one the successor published;
+// otherwise L.act = 1 (the serial walk repairs). One memory round trip when
+// the runs fit one pass (every word loaded at once, the entries exchanged in
+// LDS); tid 0 also loads the epoch and the incoming-carry snapshot (L.cinc).
+// The entry of the run or piece at flat index f in this call, NONE when it has
+// none: a piece exists only when its run agreed to the split (the run's
+// R_SPLIT, written by this call's run: R_H of an unused piece is stale).
+XYWS_DEV uint64_t entry_of(const run_params& P, uint64_t f) {
+  // (both loads unconditional: no branch, no wait between them)
+  const uint64_t h = st_load(P.rec + f * R_WORDS + R_H);
+  const uint64_t sp = st_load(P.rec + (f & ~1ull) * R_WORDS + R_SPLIT);
+  return ((f & 1) && sp == NONE) ? NONE : h;
+}
+
 template <class G>
 XYWS_DEV void finish_fast(const run_params& P, lds_t<G>& L, uint32_t tid) {
-  const uint64_t E = L.E;
-  // Fast path (every run with an entry landed exactly on its successor's
-  // entry: the usual case): frame counts, descriptor ordinals and the final
-  // state by a block-wide scan over the run records, no serial walk. A run is
-  // good when its record is this call's, its successor wait did not time out,
-  // its chain landed on the successor's entry and that entry is the one the
-  // successor published.
-  {
-    uint64_t* scr = reinterpret_cast<uint64_t*>(L.seg);  // scratch: wave totals
-    // every run's entry, for the successor check (in LDS when it fits)
-    constexpr bool HS_LDS = G::SEG >= 1024 + 8 * MAX_RUNS;
-    uint64_t* hs = reinterpret_cast<uint64_t*>(L.seg + 1024);
-    if constexpr (HS_LDS) {
-      for (uint32_t r = tid; r < P.nruns; r += G::NT) hs[r] = st_load(P.rec + (uint64_t)r * R_WORDS + R_H);
-      __syncthreads();
-    }
-    const uint32_t lane = tid & 63u, wave = tid >> 6;
-    uint64_t carry = 0;
-    uint32_t bad = 0, stale = 0, last = 0;
-    bool has = false;
-    cstate fsl;  // final state of this thread's last visible run
-    for (uint32_t t0 = 0; t0 < P.nruns; t0 += G::NT) {
-      const uint32_t r = t0 + tid;
-      const uint64_t* rec = P.rec + (uint64_t)r * R_WORDS;
-      // every word this pass needs is loaded at once (one memory round trip
-      // instead of three dependent ones; the final state of the last visible
-      // run comes from its own thread)
-      uint64_t h = NONE, cw = 0, okw = OK_BIT, ep = E, hn = NONE;
-      cstate fs;
-      if (r < P.nruns) {
-        h = HS_LDS ? hs[r] : st_load(rec + R_H);
-        cw = st_load(rec + R_CNT);
-        okw = st_load(rec + R_OK);
-        ep = st_load(rec + R_EP);
-        hn = st_load(rec + R_HN);
-        fs = get_state(rec + R_F0);
-      }
-      const bool vis = r < P.nruns && (r == 0 || h != NONE);
-      const uint64_t cnt = vis ? cw : 0;
-      if (vis) {
-        const uint64_t succ = okw >> 32;
-        if (ep != E) stale = 1;
-        if (!(okw & OK_BIT) || (okw & TMO_BIT) || ep != E) bad = 1;
-        if (succ < P.nruns && hn != (HS_LDS ? hs[succ] : st_load(P.rec + succ * R_WORDS + R_H))) bad = 1;
-        last = r;
-        fsl = fs;
-        has = true;
-      }
-      uint64_t x = cnt;  // wave inclusive scan
+  uint64_t* scr = reinterpret_cast<uint64_t*>(L.seg);  // scratch: wave totals
+  // every run's entry, for the successor check (in LDS when it fits)
+  constexpr bool HS_LDS = G::SEG >= 1024 + 16 * MAX_RUNS;
+  uint64_t* hs = reinterpret_cast<uint64_t*>(L.seg + 1024);
+  const bool one = HS_LDS && P.nflat <= G::NT;  // one pass: entries exchanged after the loads
+  if (HS_LDS && !one) {
+    for (uint32_t r = tid; r < P.nflat; r += G::NT) hs[r] = entry_of(P, r);
+  }
+  // this thread's record of the first pass: its loads go out together with
+  // lane 0's epoch and carry loads (one memory round trip before the scan)
+  struct rec_t {
+    uint64_t h, cw, okw, ep, hn;
+    cstate fs;
+  };
+  auto load_rec = [&](uint32_t r, rec_t& x) {
+    const uint64_t* rec = P.rec + (uint64_t)r * R_WORDS;
+    x.cw = st_load(rec + R_CNT);
+    x.okw = st_load(rec + R_OK);
+    x.ep = st_load(rec + R_EP);
+    x.hn = st_load(rec + R_HN);
+    x.fs = get_state(rec + R_F0);
+    x.h = (HS_LDS && !one) ? hs[r] : entry_of(P, r);  // (last: the select waits for it)
+  };
+  // (every load goes out before the first LDS write or select that waits:
+  // interleaved, each would wait for the ones before it)
+  uint64_t c[9];
+  if (tid == 0) {
+    c[8] = st_load(reinterpret_cast<const uint64_t*>(P.head + HEAD_EPOCH));
 #pragma unroll
-      for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint64_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-      }
-      if (lane == 63) scr[wave] = x;
-      __syncthreads();
-      uint64_t wb = 0, tot = 0;
-      for (uint32_t w = 0; w < G::NT / 64; w++) {
-        const uint64_t v = scr[w];
-        if (w < wave) wb += v;
-        tot += v;
-      }
-      if (vis) {
-        uint64_t* rw = P.rec + (uint64_t)r * R_WORDS;
-        st_store(rw + R_EFROM, h);
-        st_store(rw + R_ECNT, cnt);
-        st_store(rw + R_EORD, carry + wb + x - cnt);
-        st_store(rw + R_ECARRY, r == 0 ? 1u : 0u);
-      }
-      carry += tot;
-      __syncthreads();
-    }
-    // a record not written by this call: a run did not complete (reported;
-    // the outputs of this call are invalid)
-    if (__syncthreads_or(stale) && tid == 0) atomicOr(P.head + 1, 4u);
-    const bool any_bad = __syncthreads_or(bad);
-    if (tid == 0) L.aux1 = 0;
-    __syncthreads();
-    if (last) atomicMax(reinterpret_cast<unsigned long long*>(&L.aux1), (unsigned long long)last);
-    __syncthreads();
-    if (!any_bad) {
-      if (tid == 0) L.aux2 = carry;
-      if (has && last == L.aux1) L.S = fsl;
-      __syncthreads();
-    }
-    if (tid == 0) L.act = any_bad ? 1u : 0u;
-    __syncthreads();
+    for (int i = 0; i < 8; i++) c[i] = st_load(reinterpret_cast<const uint64_t*>(P.cin) + i);
   }
+  rec_t x0;
+  x0.h = NONE; x0.cw = 0; x0.okw = OK_BIT; x0.ep = 0; x0.hn = NONE;
+  if (tid < P.nflat) load_rec(tid, x0);
   if (tid == 0) {
-    if (L.act) {
-      __hip_atomic_store(P.head + HEAD_REPAIR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    L.E = c[8] + 1;
+#pragma unroll
+    for (int i = 0; i < 8; i++) reinterpret_cast<uint64_t*>(&L.cinc)[i] = c[i];
+  }
+  __syncthreads();
+  const uint64_t E = L.E;
+  const uint32_t lane = tid & 63u, wave = tid >> 6;
+  uint64_t carry = 0;
+  uint32_t bad = 0, stale = 0, last = 0;
+  bool has = false;
+  cstate fsl;  // final state of this thread's last visible run
+  for (uint32_t t0 = 0; t0 < P.nflat; t0 += G::NT) {
+    const uint32_t r = t0 + tid;
+    rec_t x;
+    if (t0 == 0) {
+      x = x0;
     } else {
-      xyws_carry cin;
-      for (int i = 0; i < 8; i++)
-        reinterpret_cast<uint64_t*>(&cin)[i] = st_load(reinterpret_cast<const uint64_t*>(P.cin) + i);
-      write_outputs(P, cin, L.aux2, L.S);
+      x.h = NONE; x.cw = 0; x.okw = OK_BIT; x.ep = E; x.hn = NONE;
+      if (r < P.nflat) load_rec(r, x);
     }
+    if (r >= P.nflat) x.ep = E;
+    if (one) {
+      if (r < P.nflat) hs[r] = x.h;
+      __syncthreads();
+    }
+    const uint64_t h = x.h, okw = x.okw, ep = x.ep, hn = x.hn;
+    const bool vis = r < P.nflat && (r == 0 || h != NONE);
+    const uint64_t cnt = vis ? x.cw : 0;
+    if (vis) {
+      const uint64_t succ = okw >> 32;
+      if (ep != E) stale = 1;
+      if (!(okw & OK_BIT) || (okw & TMO_BIT) || ep != E) bad = 1;
+      if (succ < P.nflat && hn != (HS_LDS ? hs[succ] : entry_of(P, succ))) bad = 1;
+      last = r;
+      fsl = x.fs;
+      has = true;
+    }
+    uint64_t xs = cnt;  // wave inclusive scan
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(xs, o, 64);
+      if (lane >= o) xs += y;
+    }
+    if (lane == 63) scr[wave] = xs;
+    __syncthreads();
+    uint64_t wb = 0, tot = 0;
+    for (uint32_t w = 0; w < G::NT / 64; w++) {
+      const uint64_t v = scr[w];
+      if (w < wave) wb += v;
+      tot += v;
+    }
+    if (vis && XYWS_EXP_FINISH != 3) {
+      uint64_t* rw = P.rec + (uint64_t)r * R_WORDS;
+      st_store(rw + R_EFROM, h);
+      st_store(rw + R_ECNT, cnt);
+      st_store(rw + R_EORD, carry + wb + xs - cnt);
+      st_store(rw + R_ECARRY, r == 0 ? 1u : 0u);
+    }
+    carry += tot;
+    __syncthreads();
   }
+  // a record not written by this call: a run did not complete (reported; the
+  // outputs of this call are invalid)
+  if (__syncthreads_or(stale) && tid == 0) atomicOr(P.head + 1, 4u);
+  const bool any_bad = __syncthreads_or(bad);
+  if (tid == 0) L.aux1 = 0;
+  __syncthreads();
+  if (last) atomicMax(reinterpret_cast<unsigned long long*>(&L.aux1), (unsigned long long)last);
+  __syncthreads();
+  if (!any_bad) {
+    if (tid == 0) L.aux2 = carry;
+    if (has && last == L.aux1) L.S = fsl;
+  }
+  if (tid == 0) L.act = any_bad ? 1u : 0u;
+  __syncthreads();
 }
 
-// End of a run (every workgroup, whatever its path): the records it wrote
-// (lane 0, sc1) have landed, then one done-count add; the run whose add comes
-// last finishes the call.
+// Decode the run or piece at L.self after its prologue (whole workgroup): the
+// chain from the entry state in L, writing from wlo (segment ss0, already in
+// LDS when in_lds), then its results in its record. rng_end: the end of its
+// range (NONE: the batch end); victim: it answers steal requests.
 template <class G>
-XYWS_DEV void end_of_run(const run_params& P, lds_t<G>& L, uint32_t tid) {
-  if (tid == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    L.ticket = atomicAdd(P.head + HEAD_DONE, 1u) + 1 == P.nruns ? 1u : 0u;
-  }
-  __syncthreads();
-  if (L.ticket) finish_fast<G>(P, L, tid);
-}
-
-// ---------------------------------------------------------------- kernels
-template <class G>
-__global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
-  lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
-  const uint32_t tid = threadIdx.x;
-  if (tid == 0) {
-    L.ticket = atomicAdd(P.head, 1u);
-    L.E = st_load(reinterpret_cast<const uint64_t*>(P.head + HEAD_EPOCH)) + 1;
-  }
-  __syncthreads();
-  const uint32_t run = uniform32(L.ticket);
-  if (run >= P.nruns) return;
-  uint64_t* rec = P.rec + (uint64_t)run * R_WORDS;
-  if (tid == 0) st_store(rec + R_ECNT, 0);  // no descriptors unless k_stream_finish plans them
-  const uint64_t rng_end = run + 1 < P.nruns ? (uint64_t)(run + 1) * P.rbytes : NONE;
-  seg_io<G> io;
-  uint64_t wlo, ss0;
-  bool in_lds = false;
-  if (run == 0) {
-    if (tid == 0) {
-      // snapshot of the incoming carry for k_stream_finish / k_stream_emit
-      // (the caller's carry may alias the carry out, which finish writes)
-      xyws_carry cz;
-      if (P.cin_user) {
-        cz = *P.cin_user;
-      } else {
-        for (int i = 0; i < 64; i++) reinterpret_cast<uint8_t*>(&cz)[i] = 0;
-      }
-      // (sc1 stores: the call's finishing run reads them, on any CU)
-      for (int i = 0; i < 8; i++)
-        st_store(reinterpret_cast<uint64_t*>(P.cin) + i, reinterpret_cast<const uint64_t*>(&cz)[i]);
-      uint64_t c0;
-      L.S = initial_state(P, &cz, c0);
-      L.cnt = c0;
-      st_store(rec + R_H, P.lo);
-      st_store(rec + R_W, P.lo);
-      put_state(rec + R_S0, L.S);
-      st_store(rec + R_HEAD, c0);
-    }
-    wlo = P.lo;
-    ss0 = 0;
-  } else {
-    // claim the own prologue (a predecessor that finds it unclaimed gives up
-    // on this run instead of waiting for a workgroup that may not be running)
-    if (tid == 0) granule_store(P.flags + 2 * (uint64_t)run, flag_claimed(L.E), 0);
-    prologue<G>(P, L, io, tid, run);
-    if (L.aux2 == NONE) {  // no entry: the chain of an earlier run covers this range
-      end_of_run<G>(P, L, tid);
-      return;
-    }
-    wlo = uniform64(L.aux2);
-    // the chain starts in the scanned segment (usual) or on the grid after it
-    const uint64_t a1 = uniform64(L.aux1);
-    ss0 = a1 + (wlo - a1) / G::SEG * G::SEG;
-    in_lds = ss0 == a1;
-    // (the next segment's loads were issued before the scan)
-    if (in_lds && ss0 + G::SEG < P.hi && io.pf != ss0 + G::SEG) io.issue(P, ss0 + G::SEG, tid);
-  }
+XYWS_DEV void decode_range(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint64_t ss0, bool in_lds,
+                           uint64_t wlo, uint64_t rng_end, bool victim) {
   if (tid == 0) {
     L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.tmo = 0; L.first_after = NONE;
-    if (run == 0) L.dense = 0;
-    L.known = rng_end == NONE;
-    L.hn = NONE; L.Wn = NONE; L.succ = P.nruns; L.scan_j = run + 1;
+    L.known = 0;
+    L.rng_end = rng_end;
+    L.victim = victim ? 1u : 0u;
+    L.hn = NONE; L.Wn = NONE; L.succ = P.nflat;
+    // (a run's own piece comes first when it is split while decoding)
+    L.scan_j = L.self + 1;
   }
   __syncthreads();
-  uint64_t t1 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
-  run_chain(P, L, io, tid, ss0, in_lds, wlo, rng_end, run);
+  const uint64_t t1 = stats_on(P) ? __builtin_amdgcn_s_memtime() : 0;
+  run_chain(P, L, io, tid, ss0, in_lds, wlo);
   if (tid == 0) {
-    uint64_t* rec = P.rec + (uint64_t)run * R_WORDS;
-    const bool ok = !L.tmo && (L.succ >= P.nruns || (L.past && L.ok));
+    if (L.victim) {  // (the chain ended without a successor lookup)
+      close_split(P, P.split + 2 * (L.self >> 1), L.E);
+      L.victim = 0;
+    }
+    uint64_t* rec = P.rec + L.self * R_WORDS;
+    const bool ok = !L.tmo && (L.succ >= P.nflat || (L.past && L.ok));
     st_store(rec + R_OK, (ok ? OK_BIT : 0) | (L.tmo ? TMO_BIT : 0) | ((uint64_t)L.succ << 32));
     st_store(rec + R_HN, L.hn);
     st_store(rec + R_WN, L.Wn);
@@ -1690,20 +1787,191 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
     st_store(rec + R_FIRST, L.first_after);
     put_state(rec + R_F0, L.S);
     st_store(rec + R_EP, L.E);
+    if (stats_on(P)) st_store(rec + R_T2, __builtin_amdgcn_s_memrealtime());
     if (!ok) stat_add(P, ST_BAD, 1);
     if (L.tmo) stat_add(P, ST_GIVEUP, 1);
     stat_add(P, ST_FRAMES, L.cnt);
     if (stats_on(P)) stat_add(P, ST_T_MAIN, __builtin_amdgcn_s_memtime() - t1);
   }
-  end_of_run<G>(P, L, tid);
+  __syncthreads();
 }
 
-// The next run after r with an entry (lane 0; every prologue is published by
-// now), or nruns.
+// A workgroup whose own run is done steals (whole workgroup): it asks the run
+// with the most segments left (read from the runs' progress words) for the
+// tail of its range. Returns the run that agreed (the piece starts at segment
+// L.aux1 of its range), or NONE32 when no run has enough left.
+template <class G>
+XYWS_DEV uint32_t steal_piece(const run_params& P, lds_t<G>& L, uint32_t tid) {
+  const uint64_t E = L.E;
+  const uint64_t min_left = (P.opts & XYWS_OPT_TEST_STEAL) ? 3 : XYWS_STEAL_MIN_LEFT;
+  for (uint32_t attempt = 0; attempt < 2 * P.nruns; attempt++) {
+    if (tid == 0) L.aux0 = 0;
+    __syncthreads();
+    for (uint32_t r = tid; r < P.nruns; r += G::NT) {
+      const uint64_t sw = st_load(P.split + 2 * r), pw = st_load(P.prog + r);
+      if (split_is(sw, E, SP_FREE) && (pw >> 24) == (E & ((1ull << 40) - 1))) {
+        const uint64_t rs = (uint64_t)r * P.rbytes;
+        const uint64_t re = r + 1 < P.nruns ? rs + P.rbytes : P.hi;
+        const uint64_t nseg = (re - rs + G::SEG - 1) / G::SEG, i = pw & 0xFFFFFFu;
+        const uint64_t left = nseg > i + 1 ? nseg - i - 1 : 0;
+        if (left >= min_left)
+          atomicMax(reinterpret_cast<unsigned long long*>(&L.aux0), (unsigned long long)((left << 32) | (P.nruns - r)));
+      }
+    }
+    __syncthreads();
+    const uint64_t best = L.aux0;
+    if (!best) return NONE32;
+    const uint32_t v = P.nruns - (uint32_t)(best & 0xFFFFFFFFu);
+    if (tid == 0) {
+      L.act = 0;
+      uint64_t* sw = P.split + 2 * (uint64_t)v;
+      const unsigned long long fr = split_word(E, SP_FREE, 0);
+      stat_add(P, ST_STEAL_REQ, 1);
+      if (atomicCAS(reinterpret_cast<unsigned long long*>(sw), fr, (unsigned long long)split_word(E, SP_REQ, 0)) == fr) {
+        // the run answers within a segment or two (it polls every segment)
+        uint32_t it = 0;
+        uint64_t w = split_word(E, SP_REQ, 0);
+        while (split_is(w, E, SP_REQ) && it < SPIN) {
+          __builtin_amdgcn_s_sleep(2);
+          w = st_load(sw);
+          it++;
+        }
+        if (split_is(w, E, SP_ACC)) {
+          L.act = 1;
+          L.aux1 = split_seg(w);
+        } else if (split_is(w, E, SP_REQ)) {
+          atomicOr(P.head + 1, 2u);  // (bounded wait timed out: reported, the run is left alone)
+        }
+      }
+    }
+    __syncthreads();
+    if (L.act) return v;
+  }
+  return NONE32;
+}
+
+// ---------------------------------------------------------------- kernels
+// One workgroup per run (ticket order). After its own run a workgroup takes
+// pieces of slower runs (steal_piece) until none is worth taking; the run /
+// piece loop keeps one copy of the prologue and of the chain in the kernel.
+template <class G>
+__global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
+  lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
+  const uint32_t tid0 = threadIdx.x, tid = tid0;
+  if (tid == 0) {
+    L.ticket = atomicAdd(P.head, 1u);
+    L.E = st_load(reinterpret_cast<const uint64_t*>(P.head + HEAD_EPOCH)) + 1;
+  }
+  __syncthreads();
+  const uint32_t run = uniform32(L.ticket);
+  if (run >= P.nruns) return;
+  const bool steal = (P.opts & (XYWS_OPT_STEAL | XYWS_OPT_TEST_STEAL)) != 0;
+  {
+    const uint64_t rs = (uint64_t)run * P.rbytes;
+    uint64_t* rec = P.rec + 2 * (uint64_t)run * R_WORDS;
+    if (tid == 0) {
+      // no descriptors unless k_stream_finish plans them (the run and its piece)
+      st_store(rec + R_ECNT, 0);
+      st_store(rec + R_WORDS + R_ECNT, 0);
+      st_store(rec + R_SPLIT, NONE);
+      // the run can be asked for the tail of its range from now on
+      st_store(P.split + 2 * (uint64_t)run, split_word(L.E, steal ? SP_FREE : SP_CLS, 0));
+      L.split_poll[0] = split_word(L.E, SP_FREE, 0);
+      L.split_e = NONE;
+      L.self = 2 * (uint64_t)run;
+      L.rs = rs;
+      if (stats_on(P)) st_store(rec + R_T0, __builtin_amdgcn_s_memrealtime());
+      if (run == 0) {
+        // snapshot of the incoming carry for k_stream_finish / k_stream_emit
+        // (the caller's carry may alias the carry out, which finish writes)
+        xyws_carry cz;
+        if (P.cin_user) {
+          cz = *P.cin_user;
+        } else {
+          for (int i = 0; i < 64; i++) reinterpret_cast<uint8_t*>(&cz)[i] = 0;
+        }
+        // (sc1 stores: another CU's finish reads them)
+        for (int i = 0; i < 8; i++)
+          st_store(reinterpret_cast<uint64_t*>(P.cin) + i, reinterpret_cast<const uint64_t*>(&cz)[i]);
+        uint64_t c0;
+        L.S = initial_state(P, &cz, c0);
+        L.cnt = c0;
+        L.dense = 0;
+        st_store(rec + R_H, P.lo);
+        st_store(rec + R_W, P.lo);
+        put_state(rec + R_S0, L.S);
+        st_store(rec + R_HEAD, c0);
+        granule_store(P.flags, flag_published(L.E), P.lo | granule_tag(L.E));
+      } else {
+        // claim the own prologue (a predecessor that finds it unclaimed gives
+        // up on this run instead of waiting for a workgroup that may not be
+        // running)
+        granule_store(P.flags + 4 * (uint64_t)run, flag_claimed(L.E), 0);
+      }
+      // the item decoded first: the own run
+      L.ib = rs;
+      L.ie = rs + P.rbytes;
+      // (test mode: every fourth run starts late, so that others finish first
+      // and take pieces of it whatever the hardware's own imbalance)
+      if ((P.opts & XYWS_OPT_TEST_STEAL) && (run & 3u) == 1u)
+        for (int i = 0; i < 24; i++) __builtin_amdgcn_s_sleep(127);
+    }
+  }
+  __syncthreads();
+  for (;;) {
+    seg_io<G> io;  // (per item: no prefetch registers live across the steal)
+    // (an opaque copy of the lane index per item: hipcc would otherwise hoist
+    // the lane address math of the chain out of this loop and spill in it)
+    uint32_t tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const uint64_t self = uniform64(L.self);
+    const bool own = !(self & 1);
+    const uint64_t rb = uniform64(L.ib), re = uniform64(L.ie);
+    const uint64_t rng_end = re < P.hi ? re : NONE;
+    uint64_t wlo = P.lo, ss0 = 0;
+    bool in_lds = false, entry = true;
+    if (self != 0) {
+      prologue<G>(P, L, io, tid, self, rb, re);
+      entry = L.aux2 != NONE;  // (no entry: the chain of an earlier run covers this range)
+      wlo = uniform64(L.aux2);
+      // the chain starts in the scanned segment (usual) or on the grid after it
+      const uint64_t a1 = uniform64(L.aux1);
+      ss0 = a1 + (wlo - a1) / G::SEG * G::SEG;
+      in_lds = ss0 == a1;
+      // (the next segment's loads were issued before the scan)
+      if (entry && in_lds && ss0 + G::SEG < P.hi && io.pf != ss0 + G::SEG) io.issue(P, ss0 + G::SEG, tid);
+    }
+    if (tid == 0 && stats_on(P)) st_store(P.rec + self * R_WORDS + R_T1, __builtin_amdgcn_s_memrealtime());
+    if (entry) {
+      decode_range<G>(P, L, io, tid, ss0, in_lds, wlo, rng_end, own && steal);
+      if (tid == 0 && own) st_store(P.rec + self * R_WORDS + R_SPLIT, L.split_e);
+    } else if (tid == 0 && own) {
+      close_split(P, P.split + self, L.E);
+    }
+    if (!steal) break;
+    // the next item: a piece of a slower run
+    const uint32_t v = steal_piece<G>(P, L, tid);
+    if (v == NONE32) break;
+    if (tid == 0) {
+      const uint64_t vs = (uint64_t)v * P.rbytes;
+      L.self = 2 * (uint64_t)v + 1;
+      L.ib = vs + L.aux1 * G::SEG;
+      L.ie = v + 1 < P.nruns ? vs + P.rbytes : P.hi;
+      L.rs = L.ib;
+      L.split_e = NONE;
+      if (stats_on(P)) st_store(P.rec + L.self * R_WORDS + R_T0, __builtin_amdgcn_s_memrealtime());
+    }
+    __syncthreads();
+  }
+}
+
+// The next run or piece after flat index r with an entry (lane 0; every
+// prologue is published by now), or nflat.
 XYWS_DEV uint64_t next_visible(const run_params& P, uint64_t r) {
-  for (uint64_t j = r + 1; j < P.nruns; j++)
-    if (st_load(P.rec + j * R_WORDS + R_H) != NONE) return j;
-  return P.nruns;
+  for (uint64_t j = r + 1; j < P.nflat; j++)
+    if (entry_of(P, j) != NONE) return j;
+  return P.nflat;
 }
 
 // The piece of run r as its workgroup recorded it (lane 0). Its hand-over is
@@ -1723,7 +1991,7 @@ XYWS_DEV void load_piece(const run_params& P, walk_t& w, uint64_t r) {
   w.succ = okw >> 32;
   w.tmo = (okw & TMO_BIT) ? 1u : 0u;
   w.ok = (okw & OK_BIT) ? 1u : 0u;
-  if (w.ok && w.succ < P.nruns && st_load(rec + R_HN) != st_load(P.rec + w.succ * R_WORDS + R_H)) w.ok = 0;
+  if (w.ok && w.succ < P.nflat && st_load(rec + R_HN) != entry_of(P, w.succ)) w.ok = 0;
 }
 
 // Set up a chase from state S with the given successor limits (lane 0).
@@ -1735,39 +2003,35 @@ XYWS_DEV void chain_start(lds_t<G>& L, const cstate& S, uint64_t hn, uint64_t Wn
   L.known = 1; L.cnt = 0; L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.dense = 0; L.tmo = 0;
   L.first_after = NONE;
   L.best = 0;
+  L.rng_end = NONE;
+  L.victim = 0;
 }
 
 // Walk the runs from run 0 along their successors, repairing every boundary
 // whose chain did not land on the successor's entry, then the frame count, the
 // carry and the descriptor plan (one workgroup; every run has exited).
+// Serial walk with repairs (whole workgroup; k_stream_finish calls it when the
+// fast path found a bad hand-over). Lane 0 keeps the current chain piece in
+// L.wk: the run whose descriptor plan it fills (r, efrom, ecarry), its frames
+// (cnt; tail = those past the successor's entry), its final state F, its
+// write limit, and how it hands over (ok / tmo / succ).
+//  * tmo (the run gave up on a successor that had not started): bridge from
+//    F, writing from the write limit, up to the next run with an entry; the
+//    bridge's frames join the piece.
+//  * !ok (the chain missed the successor's entry): undo the successor's run
+//    (replaying its own chain: XOR is an involution and a chain never writes
+//    its own header bytes), redo it from F, writing from the write limit; the
+//    redo is the next piece.
+//  * ok: the successor's own record is the next piece.
 template <class G>
-__global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
-  lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
-  const uint32_t tid = threadIdx.x;
+XYWS_DEV void finish_walk(const run_params& P, lds_t<G>& L, uint32_t tid) {
   seg_io<G> io;
-  const uint64_t E = st_load(reinterpret_cast<const uint64_t*>(P.head + HEAD_EPOCH)) + 1;
-  if (tid == 0) L.act = __hip_atomic_load(P.head + HEAD_REPAIR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  if (L.act) {
-  // Serial walk with repairs. Lane 0 keeps the current chain piece in L.wk:
-  // the run whose descriptor plan it fills (r, efrom, ecarry), its frames
-  // (cnt; tail = those past the successor's entry), its final state F, its
-  // write limit, and how it hands over (ok / tmo / succ).
-  //  * tmo (the run gave up on a successor that had not started): bridge from
-  //    F, writing from the write limit, up to the next run with an entry; the
-  //    bridge's frames join the piece.
-  //  * !ok (the chain missed the successor's entry): undo the successor's run
-  //    (replaying its own chain: XOR is an involution and a chain never writes
-  //    its own header bytes), redo it from F, writing from the write limit; the
-  //    redo is the next piece.
-  //  * ok: the successor's own record is the next piece.
   if (tid == 0) {
     L.aux2 = 0;
     load_piece(P, L.wk, 0);
   }
   __syncthreads();
-  for (uint32_t guard = 0; guard <= 4 * P.nruns + 4; guard++) {
+  for (uint32_t guard = 0; guard <= 4 * P.nflat + 4; guard++) {
     if (tid == 0) {
       walk_t& w = L.wk;
       if (w.tmo) {
@@ -1775,8 +2039,8 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
         w.succ = sj;
         w.act = 4;
         stat_add(P, ST_BRIDGE, 1);
-        chain_start(L, w.F, sj < P.nruns ? st_load(P.rec + sj * R_WORDS + R_H) : NONE,
-                    sj < P.nruns ? st_load(P.rec + sj * R_WORDS + R_W) : NONE, sj);
+        chain_start(L, w.F, sj < P.nflat ? st_load(P.rec + sj * R_WORDS + R_H) : NONE,
+                    sj < P.nflat ? st_load(P.rec + sj * R_WORDS + R_W) : NONE, sj);
       } else {
         uint64_t* rec = P.rec + w.r * R_WORDS;
         st_store(rec + R_EFROM, w.efrom);
@@ -1784,7 +2048,7 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
         st_store(rec + R_EORD, L.aux2);
         st_store(rec + R_ECARRY, w.ecarry);
         L.aux2 += w.cnt;
-        if (w.succ >= P.nruns) {
+        if (w.succ >= P.nflat) {
           w.act = 0;  // done
           L.S = w.F;
         } else if (w.ok) {
@@ -1806,7 +2070,7 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
       // bridge: the chain from where the run stopped to the next entry
       const uint64_t wp = L.wk.wlim;
       io.pf = NONE;
-      run_chain(P, L, io, tid, wp & ~15ull, false, wp, NONE, 0);
+      run_chain(P, L, io, tid, wp & ~15ull, false, wp);
       __threadfence();
       __syncthreads();
       if (tid == 0) {
@@ -1815,7 +2079,7 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
         w.tail = L.tail;
         w.first = L.first_after;
         w.F = L.S;
-        w.ok = w.succ >= P.nruns || (L.past && L.ok);
+        w.ok = w.succ >= P.nflat || (L.past && L.ok);
         w.wlim = L.Wn;
         w.tmo = 0;
       }
@@ -1828,7 +2092,7 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
     const uint64_t W = st_load(rs + R_W);
     const uint64_t hn = L.hn, Wn = L.Wn, succ = L.succ;
     io.pf = NONE;
-    run_chain(P, L, io, tid, W & ~15ull, false, W, NONE, 0);
+    run_chain(P, L, io, tid, W & ~15ull, false, W);
     __threadfence();  // the undo's stores are visible to the redo's loads
     __syncthreads();
     // redo from the exact state, same successor, from our write limit
@@ -1838,7 +2102,7 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
     }
     __syncthreads();
     io.pf = NONE;
-    run_chain(P, L, io, tid, wp & ~15ull, false, wp, NONE, 0);
+    run_chain(P, L, io, tid, wp & ~15ull, false, wp);
     __threadfence();
     __syncthreads();
     if (tid == 0) {
@@ -1853,24 +2117,36 @@ __global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
       w.F = L.S;
       w.succ = L.succ;
       w.tmo = (ws & TMO_BIT) ? 1u : 0u;
-      w.ok = !w.tmo && (L.succ >= P.nruns || (L.past && L.ok));
+      w.ok = !w.tmo && (L.succ >= P.nflat || (L.past && L.ok));
       w.wlim = L.Wn;
     }
     __syncthreads();
   }
-  }  // serial walk with repairs
-  if (L.act && tid == 0) {
-    xyws_carry cin;
-    for (int i = 0; i < 8; i++) reinterpret_cast<uint64_t*>(&cin)[i] = st_load(reinterpret_cast<const uint64_t*>(P.cin) + i);
-    write_outputs(P, cin, L.aux2, L.S);
-  }
-  // every run has exited: the ticket and the done count start the next call
-  // at zero; the epoch word advances (this call's entry granules read as stale
-  // from now on)
+}
+
+// Walk the runs from run 0 along their successors, repairing every boundary
+// whose chain did not land on the successor's entry, then the frame count, the
+// carry and the descriptor plan (one workgroup; every run has exited).
+template <class G>
+__global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
+  lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
+  const uint32_t tid = threadIdx.x;
+#if XYWS_EXP_FINISH == 2  // (timing experiment only: no fast path)
+  if (tid == 0) { L.E = st_load(reinterpret_cast<const uint64_t*>(P.head + HEAD_EPOCH)) + 1; L.act = 0; L.aux2 = 0; }
+  __syncthreads();
+#else
+  finish_fast<G>(P, L, tid);
+#endif
+  const uint64_t E = L.E;
+#if XYWS_EXP_FINISH == 0
+  if (L.act) finish_walk<G>(P, L, tid);
+#endif
   if (tid == 0) {
+    if (XYWS_EXP_FINISH != 4) write_outputs(P, &L.cinc, L.aux2, L.S);
+    // every run has exited: the ticket starts the next call at zero; the
+    // epoch word advances (this call's entry granules read as stale from now on)
     P.head[0] = 0;
-    P.head[HEAD_DONE] = 0;
-    P.head[HEAD_REPAIR] = 0;
     st_store(reinterpret_cast<uint64_t*>(P.head + HEAD_EPOCH), E);
   }
 }
@@ -1894,7 +2170,7 @@ XYWS_DEV void write_frame(const run_params& P, uint64_t ord, uint64_t start, con
 // modified by the decode) and writes them at their ordinals.
 __global__ void __launch_bounds__(64) k_stream_emit(run_params P) {
   const uint32_t r = blockIdx.x;
-  if (threadIdx.x != 0 || r >= P.nruns) return;
+  if (threadIdx.x != 0 || r >= P.nflat) return;
   const uint64_t* rec = P.rec + (uint64_t)r * R_WORDS;
   uint64_t ord = st_load(rec + R_EORD);
   const uint64_t n = st_load(rec + R_ECNT);
@@ -1964,7 +2240,7 @@ int launch_runs(const run_params& P, hipStream_t stream) {
   if (const int rc = set_lds_attr<G>()) return rc;
   hipLaunchKernelGGL(k_stream_runs<G>, dim3(P.nruns), dim3(G::NT), lds, stream, P);
   hipLaunchKernelGGL(k_stream_finish<G>, dim3(1), dim3(G::NT), lds, stream, P);
-  if (P.frames && P.cap) hipLaunchKernelGGL(k_stream_emit, dim3(P.nruns), dim3(64), 0, stream, P);
+  if (P.frames && P.cap) hipLaunchKernelGGL(k_stream_emit, dim3(P.nflat), dim3(64), 0, stream, P);
   return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
 
@@ -1987,12 +2263,21 @@ void stream_scratch_free(stream_scratch* s) {
   s->max_runs = 0;
 }
 
-static uint64_t flags_bytes(uint64_t n) { return (16 * n + 255) & ~255ull; }
+// Scratch layout for up to `runs` runs (2 * runs flat indices):
+//   head | entry granules (16 B per flat index) | split words (16 B per run) |
+//   progress words (8 B per run) | records (R_WORDS x 8 B per flat index)
+// Everything up to the records is zeroed at allocation (epoch 0: stale).
+static uint64_t granules_bytes(uint64_t runs) { return (32 * runs + 255) & ~255ull; }
+static uint64_t split_bytes(uint64_t runs) { return (16 * runs + 255) & ~255ull; }
+static uint64_t prog_bytes(uint64_t runs) { return (8 * runs + 255) & ~255ull; }
+static uint64_t records_off(uint64_t runs) {
+  return HEAD_BYTES + granules_bytes(runs) + split_bytes(runs) + prog_bytes(runs);
+}
 
 static int scratch_grow(stream_scratch* s, uint64_t runs) {
   if (s->mem && runs <= s->max_runs) return XYWS_OK;
   const uint64_t want = runs < 64 ? 64 : runs;
-  const uint64_t bytes = HEAD_BYTES + flags_bytes(want) + want * R_WORDS * 8;
+  const uint64_t bytes = records_off(want) + 2 * want * R_WORDS * 8;
   void* m = nullptr;
   if (hipMalloc(&m, bytes) != hipSuccess) return XYWS_ERR_NOMEM;
   if (s->mem) {
@@ -2002,7 +2287,7 @@ static int scratch_grow(stream_scratch* s, uint64_t runs) {
   s->mem = m;
   s->bytes = bytes;
   s->max_runs = want;
-  return hipMemset(m, 0, HEAD_BYTES + flags_bytes(want)) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
+  return hipMemset(m, 0, records_off(want)) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
 
 int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
@@ -2020,11 +2305,11 @@ int stream_scratch_stats(stream_scratch* s, uint64_t out[XYWS_NSTATS]) {
              ? XYWS_OK : XYWS_ERR_HIP;
 }
 
-int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_runs) {
+int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_recs) {
   if (!s->mem) return XYWS_ERR_INVALID;
   if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
-  const uint64_t n = max_runs < s->max_runs ? max_runs : s->max_runs;
-  const uint8_t* rec = static_cast<const uint8_t*>(s->mem) + HEAD_BYTES + flags_bytes(s->max_runs);
+  const uint64_t n = max_recs < 2 * s->max_runs ? max_recs : 2 * s->max_runs;
+  const uint8_t* rec = static_cast<const uint8_t*>(s->mem) + records_off(s->max_runs);
   return hipMemcpy(out, rec, n * R_WORDS * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int64_t)n : XYWS_ERR_HIP;
 }
 
@@ -2072,12 +2357,16 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   P.nruns = (uint32_t)nruns;
   P.cout = cout; P.frames = frames; P.cap = cap; P.nframes = nframes;
   P.head = reinterpret_cast<uint32_t*>(m);
+  P.nflat = 2 * P.nruns;
   P.flags = reinterpret_cast<uint64_t*>(m + HEAD_BYTES);
-  P.rec = reinterpret_cast<uint64_t*>(m + HEAD_BYTES + flags_bytes(s->max_runs));
+  P.split = reinterpret_cast<uint64_t*>(m + HEAD_BYTES + granules_bytes(s->max_runs));
+  P.prog = reinterpret_cast<uint64_t*>(m + HEAD_BYTES + granules_bytes(s->max_runs) + split_bytes(s->max_runs));
+  P.rec = reinterpret_cast<uint64_t*>(m + records_off(s->max_runs));
   P.opts = opts;
-  // The ticket and the flags are zero here (zeroed at allocation, reset by
-  // k_stream_finish after every call); the error word [1] is sticky until read
-  // back. Run 0 snapshots the incoming carry into scratch.
+  // The ticket is zero here (zeroed at allocation, reset by k_stream_finish
+  // after every call); granules, split and progress words carry the epoch of
+  // the call that wrote them; the error word [1] is sticky until read back.
+  // Run 0 snapshots the incoming carry into scratch.
   if ((opts & XYWS_OPT_STATS) && hipMemsetAsync(m + 128, 0, 8 * XYWS_NSTATS, stream) != hipSuccess) return XYWS_ERR_HIP;
   P.cin_user = cin;
   P.cin = reinterpret_cast<xyws_carry*>(m + 64);
