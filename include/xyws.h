@@ -14,6 +14,18 @@
  *     example/include/common/websocket.h:110-134               xyws_decode_indexed
  *   enum class websocket_flags                               XYWS_FLAG_* (same encoding)
  *     include/xynet/http/websocket_frame_header.h:42-58
+ *   websocket_frame_header_parser (incremental, one header)  xyws_parser_* (runs the stream
+ *     include/xynet/http/websocket_frame_header.h:226-385      decoder in parse-only mode)
+ *   detail::websocket_frame_header_builder                   xyws_header_build (one header),
+ *     include/xynet/http/websocket_frame_header.h:136-175      xyws_encode_frames (batched, device)
+ *   echo_once: header{FIN|TEXT, len} + send(header, data)    xyws_encode_frames
+ *     example/websocket/websocket_echo.cpp:18-27
+ *   websocket_check_parser_result (close policy)             xyws_classify_frames
+ *     example/include/common/websocket.h:81-108
+ *   (new) FIN=0 message reassembly + UTF-8 validation        xyws_reassemble
+ *   recv_all / io_service remote-queue eventfd               xyws_arena_* (pinned recv arena,
+ *     include/xynet/socket/impl/recv_all.h:86-121              H2D -> decode -> D2H, completion
+ *     include/xynet/io_service.h:362-381                       written to an eventfd)
  *
  * The reference has no FFI of its own: it is a header-only C++20 library whose
  * templates are instantiated in the caller's translation unit. A caller (an
@@ -49,7 +61,7 @@
 extern "C" {
 #endif
 
-#define XYWS_ABI_VERSION 1
+#define XYWS_ABI_VERSION 2
 
 /* ---- status codes -------------------------------------------------------- */
 #define XYWS_OK              0
@@ -169,6 +181,117 @@ int xyws_decode_stream(xyws_ctx* ctx, void* dev_buf, uint64_t len,
                        const xyws_carry* dev_carry_in, xyws_carry* dev_carry_out,
                        xyws_frame* dev_frames, uint64_t cap, uint64_t* dev_nframes,
                        uint32_t opts, void* stream);
+
+
+/* ==== ABI 2: the rest of the frame interface ============================ */
+
+#define XYWS_NPOS UINT64_MAX /* websocket_frame_header_parser::npos (:230) */
+
+/* ---- websocket_frame_header_parser (websocket_frame_header.h:226-385) ---
+ * The reference's incremental one-header parser. parse() feeds `len` bytes
+ * (host or device memory); *consumed receives the bytes consumed in THIS call
+ * up to the end of the header, or XYWS_NPOS while the header is incomplete.
+ * Once a header completed, further input returns XYWS_NPOS until reset()
+ * (:378-384). The bytes are parsed on the device by the stream decoder in
+ * parse-only mode with a device-resident carry; parse() is synchronous on
+ * `stream` (it returns the reference's answer). result() before a header
+ * completed returns zero flags, key and length. */
+typedef struct xyws_parser xyws_parser;
+int xyws_parser_create(xyws_ctx* ctx, xyws_parser** out);
+int xyws_parser_destroy(xyws_parser* p);
+int xyws_parser_reset(xyws_parser* p);
+int xyws_parser_parse(xyws_parser* p, const void* data, uint64_t len, uint64_t* consumed, void* stream);
+int xyws_parser_result(const xyws_parser* p, uint8_t* flags, uint8_t key[4], uint64_t* length);
+
+/* ---- header build (detail::websocket_frame_header_builder, :136-175) ----
+ * One header into out[14] (host memory, no device work); returns its length
+ * H. With XYWS_FLAG_HAS_MASK the 4 key bytes are written only when `key` is
+ * non-null, as the reference builder does (:168-173); with key == NULL they
+ * are zero, which is what class websocket_frame_header's masked constructors
+ * produce (:183-202). */
+uint64_t xyws_header_build(uint8_t flags, const uint8_t* key, uint64_t len, uint8_t out[14]);
+
+/* ---- batched encode on the device (echo replies, client-role frames) ----
+ * For every frame i < n_eff (n_eff = min(n, *dev_n) when dev_n is given) of
+ * a decoded frame table, writes a reply frame = header(flags_i, len_i) +
+ * payload bytes dev_src[payload_off .. +payload_len) into dev_out, replies
+ * back to back in frame order (the iovec pair echo_once sends, as one
+ * buffer). flags_i = `flags`, or with XYWS_ENC_FRAME_OPCODE the frame's own
+ * opcode and FIN (a ping answered as a pong) plus `flags`' HAS_MASK bit.
+ * With HAS_MASK and dev_keys (4 bytes per frame, wire order) the header
+ * carries key i and the payload is masked with it (client role); with
+ * HAS_MASK and dev_keys == NULL the key bytes are zero (the reference
+ * class's form) and the payload is copied unchanged. dev_verdicts (nullable,
+ * from xyws_classify_frames) with `action_mask` (bit 1<<action) selects which
+ * frames get a reply (others: none). dev_offsets (nullable) receives n_eff+1
+ * reply offsets; *dev_out_len (nullable) the total reply bytes. Bytes past
+ * out_cap are not written (compare *dev_out_len with out_cap); payload bytes
+ * past src_len read as zero and set bit 0x100 of the device error word. */
+#define XYWS_ENC_FRAME_OPCODE 0x1u
+typedef struct xyws_verdict xyws_verdict;
+int xyws_encode_frames(xyws_ctx* ctx, const void* dev_src, uint64_t src_len,
+                       const xyws_frame* dev_frames, uint64_t n, const uint64_t* dev_n,
+                       uint8_t flags, uint32_t enc_opts, const uint8_t* dev_keys,
+                       const xyws_verdict* dev_verdicts, uint32_t action_mask,
+                       void* dev_out, uint64_t out_cap, uint64_t* dev_offsets,
+                       uint64_t* dev_out_len, void* stream);
+
+/* ---- close policy per frame (websocket_check_parser_result) -------------
+ * websocket.h:81-108 checks, in order: close frame -> 1000, FIN=0 -> 1003,
+ * unmasked -> 1008, length > max -> 1009. Here without its opcode bug (the
+ * bit-3 test `flags & WS_OP_CLOSE` there also closes on ping and pong):
+ * pings and pongs are actions of their own. Policy bits relax or tighten the
+ * reference's checks. *dev_first_close (nullable) receives the index of the
+ * first frame with a close code, or UINT64_MAX. */
+#define XYWS_ACT_DATA   0 /* text/binary/continuation frame to deliver */
+#define XYWS_ACT_PING   1 /* answer with a pong carrying the same payload */
+#define XYWS_ACT_PONG   2 /* unsolicited or answering pong: nothing to do */
+#define XYWS_ACT_CLOSE  3 /* the connection closes with close_code */
+#define XYWS_POL_FRAGMENTS  0x1u /* accept FIN=0 data frames (reassembly) instead of closing 1003 */
+#define XYWS_POL_UNMASKED   0x2u /* accept unmasked frames instead of closing 1008 */
+#define XYWS_POL_STRICT     0x4u /* RFC 6455 protocol errors (RSV, reserved opcode, fragmented or
+                                    >125-byte control frame) close 1002 (the reference accepts them) */
+struct xyws_verdict {
+  uint16_t close_code; /* 0, or the code the connection closes with */
+  uint16_t peer_code;  /* close frames: the peer's status code (1005 if none) */
+  uint8_t  action;     /* XYWS_ACT_* */
+  uint8_t  reserved[3];
+};
+int xyws_classify_frames(xyws_ctx* ctx, const void* dev_src, uint64_t src_len,
+                         const xyws_frame* dev_frames, uint64_t n, const uint64_t* dev_n,
+                         uint64_t max_payload, uint32_t policy, xyws_verdict* dev_verdicts,
+                         uint64_t* dev_first_close, void* stream);
+
+/* ---- message reassembly (FIN=0 chains) + UTF-8 validation ---------------
+ * A message is a text/binary frame followed by continuation frames up to the
+ * first one with FIN (control frames may sit between fragments and are not
+ * part of it). Every message's payload is gathered into dev_out back to back
+ * (frame payloads must be complete in dev_src: decoded, unmasked); its
+ * record goes to dev_msgs[m] in order; *dev_nmsgs receives the count. With
+ * XYWS_REASM_UTF8 every text message is validated (RFC 3629: no overlongs,
+ * surrogates or code points above U+10FFFF). A continuation outside a
+ * message is dropped and reported with XYWS_MSG_ORPHANS on the next message
+ * (bit 0x200 of the device error word if none follows). */
+#define XYWS_REASM_UTF8 0x1u
+#define XYWS_MSG_COMPLETE   0x1u /* the FIN fragment is in this batch */
+#define XYWS_MSG_UTF8_BAD   0x2u /* text message: invalid UTF-8 (a sequence cut by the end of an
+                                    incomplete message is not counted) */
+#define XYWS_MSG_INTERRUPTED 0x4u /* a new text/binary frame started before the FIN fragment */
+#define XYWS_MSG_TRUNCATED  0x8u /* the payload did not fit in out_cap */
+#define XYWS_MSG_ORPHANS    0x10u /* continuation frames without a message preceded this one */
+typedef struct xyws_message {
+  uint64_t first_frame; /* index of the text/binary frame that starts it */
+  uint64_t nframes;     /* its data frames */
+  uint64_t out_off;     /* its payload in dev_out */
+  uint64_t length;      /* total payload bytes */
+  uint32_t status;      /* XYWS_MSG_* */
+  uint8_t  opcode;      /* XYWS_FLAG_OP_TEXT or XYWS_FLAG_OP_BINARY */
+  uint8_t  reserved[3];
+} xyws_message;         /* 40 bytes */
+int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len,
+                    const xyws_frame* dev_frames, uint64_t n, const uint64_t* dev_n, uint32_t opts,
+                    void* dev_out, uint64_t out_cap, xyws_message* dev_msgs, uint64_t msg_cap,
+                    uint64_t* dev_nmsgs, void* stream);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -14,15 +14,25 @@
 //     :264-267 -> tuple<flags, mask_uint32_t, length>
 //   websocket_recv_data: parse -> result -> mask          xyws::frame_decoder::decode
 //     example/include/common/websocket.h:110-134            (a whole batch of frames per call)
+//   class websocket_frame_header :179-224                 xyws::websocket_frame_header (same ctors,
+//                                                           view(), span(); masked-ctor quirk kept)
+//   class websocket_frame_header_parser :226-385          xyws::websocket_frame_header_parser
+//     parse / length / flags / mask_uint32_t / result /     (parsed on the device, xyws_parser_*)
+//     mask / reset / npos
+//   echo_once reply build (websocket_echo.cpp:18-27)      xyws::encode_frames (batched, device)
+//   websocket_check_parser_result (websocket.h:81-108)    xyws::classify_frames (device)
 //
 // Nothing here computes on the host: every call goes through libxyws.so to
 // HIP kernels for gfx950. Buffers are caller-owned device memory (hipMalloc);
 // `stream` is a hipStream_t passed as void*. Errors throw xyws::error.
 #pragma once
 
+#include <array>
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 #include <span>
+#include <string_view>
 #include <stdexcept>
 #include <string>
 #include <tuple>
@@ -184,5 +194,140 @@ class frame_decoder {
   xyws_carry* carry_;
   std::uint32_t opts_;
 };
+
+// The calling thread's context on device 0 (what default-constructed parsers
+// use, so `websocket_frame_header_parser{}` reads as in the reference).
+inline context& default_context() {
+  thread_local context ctx(0);
+  return ctx;
+}
+
+// class websocket_frame_header (websocket_frame_header.h:179-224): a header in
+// a 14-byte array. As in the reference, the masked constructors keep the key
+// beside the header and build it with the key bytes zero (:183-202); with_key()
+// builds the RFC client-role header that carries the key.
+class websocket_frame_header {
+ public:
+  websocket_frame_header(websocket_flags flags, std::size_t data_len) noexcept {
+    len_ = static_cast<std::size_t>(
+        xyws_header_build(static_cast<std::uint8_t>(flags), nullptr, data_len, hdr_.data()));
+  }
+  websocket_frame_header(websocket_flags flags, std::span<char, 4> mask, std::size_t data_len) noexcept
+      : websocket_frame_header{flags, data_len} {
+    std::memcpy(mask_.data(), mask.data(), 4);
+  }
+  websocket_frame_header(websocket_flags flags, std::uint32_t mask, std::size_t data_len) noexcept
+      : websocket_frame_header{flags, data_len} {
+    std::memcpy(mask_.data(), &mask, 4);
+  }
+  static websocket_frame_header with_key(websocket_flags flags, std::uint32_t key, std::size_t data_len) noexcept {
+    websocket_frame_header h{flags | websocket_flags::WS_HAS_MASK, data_len};
+    std::uint8_t k[4];
+    std::memcpy(k, &key, 4);
+    h.len_ = static_cast<std::size_t>(xyws_header_build(
+        static_cast<std::uint8_t>(flags | websocket_flags::WS_HAS_MASK), k, data_len, h.hdr_.data()));
+    std::memcpy(h.mask_.data(), &key, 4);
+    return h;
+  }
+  [[nodiscard]] std::string_view view() const {
+    return {reinterpret_cast<const char*>(hdr_.data()), len_};
+  }
+  [[nodiscard]] std::span<const std::byte> span() const {
+    return {reinterpret_cast<const std::byte*>(hdr_.data()), len_};
+  }
+
+ private:
+  std::array<std::uint8_t, XYWS_MAX_FRAME_HEADER_SIZE> hdr_ = {};
+  std::array<char, 4> mask_ = {};
+  std::size_t len_ = 0;
+};
+
+// class websocket_frame_header_parser (websocket_frame_header.h:226-385). parse()
+// takes host or device bytes and returns the bytes consumed in this call up to
+// the end of the header, or npos while it is incomplete; after a complete
+// header it returns npos until reset(). The parse runs on the device (the
+// stream decoder in parse-only mode, device-resident carry); it is synchronous
+// on `stream`. Unlike the reference it can throw xyws::error (a HIP failure).
+class websocket_frame_header_parser {
+ public:
+  static constexpr std::size_t npos = static_cast<std::size_t>(-1);
+
+  websocket_frame_header_parser() : websocket_frame_header_parser(default_context()) {}
+  explicit websocket_frame_header_parser(context& ctx, void* stream = nullptr) : stream_(stream) {
+    check(xyws_parser_create(ctx.native(), &p_), "xyws_parser_create");
+  }
+  ~websocket_frame_header_parser() {
+    if (p_) xyws_parser_destroy(p_);
+  }
+  websocket_frame_header_parser(const websocket_frame_header_parser&) = delete;
+  websocket_frame_header_parser& operator=(const websocket_frame_header_parser&) = delete;
+  websocket_frame_header_parser(websocket_frame_header_parser&& o) noexcept
+      : p_(std::exchange(o.p_, nullptr)), stream_(o.stream_) {}
+
+  std::size_t parse(std::string_view str) { return parse_bytes(str.data(), str.size()); }
+  template <typename T, std::size_t Extent>
+  std::size_t parse(std::span<T, Extent> sp) {
+    const auto b = std::as_bytes(sp);
+    return parse_bytes(b.data(), b.size());
+  }
+
+  std::size_t length() const noexcept { return static_cast<std::size_t>(get().payload_len); }
+  websocket_flags flags() const noexcept { return websocket_flags(get().flags); }
+  std::uint32_t mask_uint32_t() const noexcept {
+    const xyws_frame f = get();
+    std::uint32_t m;
+    std::memcpy(&m, f.key, 4);  // wire bytes reinterpreted as a host int (:259-262)
+    return m;
+  }
+  std::tuple<websocket_flags, std::uint32_t, std::size_t> result() const noexcept {
+    return {flags(), mask_uint32_t(), length()};
+  }
+  std::array<char, 4> mask() const noexcept {
+    const xyws_frame f = get();
+    std::array<char, 4> m;
+    std::memcpy(m.data(), f.key, 4);
+    return m;
+  }
+  void reset() { check(xyws_parser_reset(p_), "xyws_parser_reset"); }
+
+ private:
+  std::size_t parse_bytes(const void* data, std::size_t len) {
+    std::uint64_t consumed = XYWS_NPOS;
+    check(xyws_parser_parse(p_, data, len, &consumed, stream_), "xyws_parser_parse");
+    return consumed == XYWS_NPOS ? npos : static_cast<std::size_t>(consumed);
+  }
+  xyws_frame get() const noexcept {
+    xyws_frame f{};
+    std::uint64_t len = 0;
+    (void)xyws_parser_result(p_, &f.flags, f.key, &len);
+    f.payload_len = len;
+    return f;
+  }
+
+  xyws_parser* p_ = nullptr;
+  void* stream_ = nullptr;
+};
+
+// Batched echo replies / client-role frames on the device (xyws_encode_frames).
+inline void encode_frames(context& ctx, std::span<const std::byte> dev_src, std::span<const xyws_frame> dev_frames,
+                          const std::uint64_t* dev_n, websocket_flags flags, std::span<std::byte> dev_out,
+                          std::uint64_t* dev_out_len, std::uint32_t enc_opts = 0,
+                          const std::uint8_t* dev_keys = nullptr, const xyws_verdict* dev_verdicts = nullptr,
+                          std::uint32_t action_mask = 0, std::uint64_t* dev_offsets = nullptr,
+                          void* stream = nullptr) {
+  check(xyws_encode_frames(ctx.native(), dev_src.data(), dev_src.size(), dev_frames.data(), dev_frames.size(), dev_n,
+                           static_cast<std::uint8_t>(flags), enc_opts, dev_keys, dev_verdicts, action_mask,
+                           dev_out.data(), dev_out.size(), dev_offsets, dev_out_len, stream),
+        "xyws_encode_frames");
+}
+
+// websocket_check_parser_result's policy per frame (xyws_classify_frames).
+inline void classify_frames(context& ctx, std::span<const std::byte> dev_src, std::span<const xyws_frame> dev_frames,
+                            const std::uint64_t* dev_n, std::uint64_t max_payload, std::uint32_t policy,
+                            xyws_verdict* dev_verdicts, std::uint64_t* dev_first_close, void* stream = nullptr) {
+  check(xyws_classify_frames(ctx.native(), dev_src.data(), dev_src.size(), dev_frames.data(), dev_frames.size(),
+                             dev_n, max_payload, policy, dev_verdicts, dev_first_close, stream),
+        "xyws_classify_frames");
+}
 
 }  // namespace xyws

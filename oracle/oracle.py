@@ -44,6 +44,28 @@ class Carry(C.Structure):
 assert C.sizeof(Frame) == 32 and C.sizeof(Carry) == 64
 
 
+class Verdict(C.Structure):
+    """Mirror of xyws_verdict (include/xyws.h)."""
+    _fields_ = [("close_code", C.c_uint16), ("peer_code", C.c_uint16), ("action", C.c_uint8),
+                ("reserved", C.c_uint8 * 3)]
+
+    def as_tuple(self):
+        return (self.close_code, self.peer_code, self.action)
+
+
+class Message(C.Structure):
+    """Mirror of xyws_message (include/xyws.h)."""
+    _fields_ = [("first_frame", C.c_uint64), ("nframes", C.c_uint64), ("out_off", C.c_uint64),
+                ("length", C.c_uint64), ("status", C.c_uint32), ("opcode", C.c_uint8),
+                ("reserved", C.c_uint8 * 3)]
+
+    def as_tuple(self):
+        return (self.first_frame, self.nframes, self.out_off, self.length, self.status, self.opcode)
+
+
+assert C.sizeof(Verdict) == 8 and C.sizeof(Message) == 40
+
+
 class SynthFrame(C.Structure):
     """Mirror of xyws_synth_frame (include/xyws_synth.h)."""
     _fields_ = [("off", C.c_uint64), ("plen", C.c_uint64), ("draw", C.c_uint64),
@@ -100,6 +122,13 @@ class Oracle:
         L.oracle_fill_mixed.argtypes = [vp, vp, u64, u64]
         L.oracle_decode_batch_mt.restype = u64
         L.oracle_decode_batch_mt.argtypes = [vp, u64, C.c_int]
+        L.oracle_encode_frames.restype = u64
+        L.oracle_encode_frames.argtypes = [vp, u64, vp, u64, u8, u32, vp, vp, u32, vp, u64, vp]
+        L.oracle_classify.argtypes = [vp, u64, vp, u64, u64, u32, vp, C.POINTER(u64)]
+        L.oracle_utf8_valid.restype = C.c_int
+        L.oracle_utf8_valid.argtypes = [vp, u64, C.c_int]
+        L.oracle_reassemble.restype = u64
+        L.oracle_reassemble.argtypes = [vp, u64, vp, u64, u32, vp, u64, vp, u64]
 
     # --- parser object (websocket_frame_header_parser) ---
     class Parser:
@@ -176,6 +205,58 @@ class Oracle:
         a[:, 30] &= 1
         a[:, 31] = 0
         return self.digest(a.reshape(-1))
+
+    # --- callers either side of the path (xyws_frames.hip semantics) ---
+    @staticmethod
+    def _frames(frames):
+        arr = (Frame * max(1, len(frames)))()
+        for i, f in enumerate(frames):
+            arr[i] = f
+        return arr
+
+    def encode_frames(self, src: np.ndarray, frames, flags, enc_opts=0, keys=None, verdicts=None,
+                      action_mask=0, out_cap=None):
+        """echo_once replies for a frame list: (reply bytes, offsets)."""
+        fr = self._frames(frames)
+        n = len(frames)
+        kb = None if keys is None else np.ascontiguousarray(np.frombuffer(bytes(keys), np.uint8))
+        vd = None
+        if verdicts is not None:
+            vd = (Verdict * max(1, n))()
+            for i, v in enumerate(verdicts):
+                vd[i] = v
+        total = self.L.oracle_encode_frames(_ptr(src), src.size, fr, n, flags, enc_opts, _ptr(kb), vd,
+                                            action_mask, None, 0, None)
+        cap = total if out_cap is None else out_cap
+        out = np.zeros(max(cap, 1), np.uint8)
+        offs = np.zeros(n + 1, np.uint64)
+        self.L.oracle_encode_frames(_ptr(src), src.size, fr, n, flags, enc_opts, _ptr(kb), vd, action_mask,
+                                    _ptr(out), cap, _ptr(offs))
+        return out[:min(cap, total)].tobytes(), offs, total
+
+    def classify(self, src: np.ndarray, frames, max_payload, policy):
+        n = len(frames)
+        fr = self._frames(frames)
+        out = (Verdict * max(1, n))()
+        first = C.c_uint64()
+        self.L.oracle_classify(_ptr(src), src.size, fr, n, max_payload, policy, out, C.byref(first))
+        return [out[i] for i in range(n)], first.value
+
+    def utf8_valid(self, data: bytes, complete=True):
+        b = np.frombuffer(bytes(data), np.uint8).copy() if data else np.zeros(1, np.uint8)
+        return bool(self.L.oracle_utf8_valid(_ptr(b), len(data), 1 if complete else 0))
+
+    def reassemble(self, src: np.ndarray, frames, opts, out_cap=None):
+        """(gathered bytes, message list)."""
+        n = len(frames)
+        fr = self._frames(frames)
+        cap_m = max(1, n)
+        msgs = (Message * cap_m)()
+        total = sum(f.payload_len for f in frames)
+        cap = total if out_cap is None else out_cap
+        out = np.zeros(max(cap, 1), np.uint8)
+        nm = self.L.oracle_reassemble(_ptr(src), src.size, fr, n, opts, _ptr(out), cap, msgs, cap_m)
+        return out, [msgs[i] for i in range(nm)]
 
     def fill_uniform(self, nframes, plen, b0, seed) -> np.ndarray:
         H = 2 + (0 if plen < 126 else (2 if plen <= 0xFFFF else 8)) + 4

@@ -14,6 +14,8 @@
  *   - detail::calc_frame_header_size         :111-126
  *   - detail::websocket_frame_header_builder :136-175
  *   - websocket_mask                         include/xynet/http/websocket_frame_mask.h:6-25
+ *   - websocket_check_parser_result's policy example/include/common/websocket.h:81-108
+ *   - echo_once's reply (header + payload)   example/websocket/websocket_echo.cpp:18-27
  * and the batch semantics this build defines on top of them: every frame of a
  * back-to-back batch parsed by a fresh parser and its payload unmasked in
  * place from phase 0, as websocket_recv_data does for one frame
@@ -295,6 +297,163 @@ void oracle_decode_indexed(uint8_t* buf, uint64_t len, const uint64_t* starts, u
     }
     if (frames) frames[i] = f;
   }
+}
+
+/* ---- the callers either side of the path (xyws_frames.hip's semantics) ---- */
+
+/* echo_once's reply for every selected frame (websocket_echo.cpp:22-26):
+ * header_build(flags_i, key_i or NULL, len_i) + payload bytes (masked with
+ * key_i when keys are given), back to back. Returns the total reply bytes;
+ * bytes past out_cap are not written; offsets (nullable) gets n + 1 entries. */
+uint64_t oracle_encode_frames(const uint8_t* src, uint64_t src_len, const xyws_frame* frames, uint64_t n,
+                              uint8_t flags, uint32_t enc_opts, const uint8_t* keys, const xyws_verdict* verd,
+                              uint32_t amask, uint8_t* out, uint64_t out_cap, uint64_t* offsets) {
+  uint64_t pos = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    if (offsets) offsets[i] = pos;
+    if (verd && !((amask >> verd[i].action) & 1u)) continue;
+    const xyws_frame* f = &frames[i];
+    uint8_t fl = flags;
+    if (enc_opts & XYWS_ENC_FRAME_OPCODE) {
+      uint8_t op = f->flags & XYWS_FLAG_OP_MASK;
+      if (op == XYWS_FLAG_OP_PING) op = XYWS_FLAG_OP_PONG;
+      fl = (uint8_t)(op | (f->flags & XYWS_FLAG_FIN) | (flags & XYWS_FLAG_HAS_MASK));
+    }
+    const uint8_t* key = (keys && (fl & XYWS_FLAG_HAS_MASK)) ? keys + 4 * i : NULL;
+    uint8_t hdr[XYWS_MAX_FRAME_HEADER_SIZE] = {0};  /* (zero key bytes without a key, as the
+                                                        class's zero-initialised array, :221) */
+    uint64_t h = oracle_header_build(hdr, fl, key, f->payload_len);
+    for (uint64_t j = 0; j < h; j++, pos++)
+      if (pos < out_cap) out[pos] = hdr[j];
+    for (uint64_t j = 0; j < f->payload_len; j++, pos++) {
+      uint64_t sp = (uint64_t)f->payload_off + j;
+      uint8_t b = sp < src_len ? src[sp] : 0;
+      if (key) b ^= key[j & 3];
+      if (pos < out_cap) out[pos] = b;
+    }
+  }
+  if (offsets) offsets[n] = pos;
+  return pos;
+}
+
+/* websocket_check_parser_result (websocket.h:81-108): close -> 1000, FIN=0 ->
+ * 1003, unmasked -> 1008, length > max -> 1009, first match wins; without its
+ * bit-3 test (`flags & WS_OP_CLOSE` is also true for ping and pong). Policy
+ * bits: XYWS_POL_FRAGMENTS skips the FIN test, XYWS_POL_UNMASKED the mask
+ * test, XYWS_POL_STRICT puts RFC protocol errors (1002) first. *first: the
+ * first closing frame, or UINT64_MAX. */
+void oracle_classify(const uint8_t* src, uint64_t src_len, const xyws_frame* frames, uint64_t n,
+                     uint64_t max_payload, uint32_t policy, xyws_verdict* out, uint64_t* first) {
+  if (first) *first = UINT64_MAX;
+  for (uint64_t i = 0; i < n; i++) {
+    const xyws_frame* f = &frames[i];
+    uint8_t op = f->flags & XYWS_FLAG_OP_MASK;
+    xyws_verdict v;
+    memset(&v, 0, sizeof v);
+    v.action = op == XYWS_FLAG_OP_PING ? XYWS_ACT_PING : op == XYWS_FLAG_OP_PONG ? XYWS_ACT_PONG : XYWS_ACT_DATA;
+    int proto = (f->status & (XYWS_ST_RSV | XYWS_ST_RESERVED_OPCODE | XYWS_ST_BAD_CONTROL)) != 0;
+    uint16_t code = 0;
+    if ((policy & XYWS_POL_STRICT) && proto) code = 1002;
+    else if (op == XYWS_FLAG_OP_CLOSE) code = 1000;
+    else if (!(f->flags & XYWS_FLAG_FIN) && !(policy & XYWS_POL_FRAGMENTS)) code = 1003;
+    else if (!(f->flags & XYWS_FLAG_HAS_MASK) && !(policy & XYWS_POL_UNMASKED)) code = 1008;
+    else if (f->payload_len > max_payload) code = 1009;
+    if (op == XYWS_FLAG_OP_CLOSE) {
+      v.action = XYWS_ACT_CLOSE;
+      uint64_t p = (uint64_t)f->payload_off;
+      v.peer_code = 1005;
+      if (f->payload_len >= 2 && p + 2 <= src_len) v.peer_code = (uint16_t)((src[p] << 8) | src[p + 1]);
+    }
+    if (code) {
+      v.close_code = code;
+      v.action = XYWS_ACT_CLOSE;
+      if (first && *first == UINT64_MAX) *first = i;
+    }
+    out[i] = v;
+  }
+}
+
+/* RFC 3629 UTF-8 over s[0, len): 1 if valid. With complete == 0 a sequence
+ * cut by the end is accepted (the message continues later). */
+int oracle_utf8_valid(const uint8_t* s, uint64_t len, int complete) {
+  uint64_t i = 0;
+  while (i < len) {
+    uint8_t c = s[i];
+    if (c < 0x80) { i++; continue; }
+    uint32_t L = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : c >= 0xC0 ? 2 : 0;
+    if (L == 0 || c == 0xC0 || c == 0xC1 || c >= 0xF5) return 0;
+    for (uint32_t d = 1; d < L; d++) {
+      if (i + d >= len) return complete ? 0 : 1;
+      uint8_t x = s[i + d];
+      if ((x & 0xC0) != 0x80) return 0;
+      if (d == 1) {
+        if (c == 0xE0 && x < 0xA0) return 0;
+        if (c == 0xED && x > 0x9F) return 0;
+        if (c == 0xF0 && x < 0x90) return 0;
+        if (c == 0xF4 && x > 0x8F) return 0;
+      }
+    }
+    i += L;
+  }
+  return 1;
+}
+
+/* Messages of a decoded batch (the semantics of xyws_reassemble): a text or
+ * binary frame opens a message, continuations join it up to the first with
+ * FIN; control frames between fragments are skipped; a continuation with no
+ * open message is dropped (XYWS_MSG_ORPHANS on the next message). Payloads
+ * are gathered into out back to back. Returns the message count. */
+uint64_t oracle_reassemble(const uint8_t* src, uint64_t src_len, const xyws_frame* frames, uint64_t n,
+                           uint32_t opts, uint8_t* out, uint64_t out_cap, xyws_message* msgs, uint64_t msg_cap) {
+  uint64_t nm = 0, pos = 0;
+  int64_t open = -1;
+  int orphans = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    const xyws_frame* f = &frames[i];
+    uint8_t op = f->flags & XYWS_FLAG_OP_MASK;
+    if (op > XYWS_FLAG_OP_BINARY) continue;
+    int64_t m;
+    if (op != XYWS_FLAG_OP_CONTINUE) {
+      if (open >= 0 && (uint64_t)open < msg_cap) msgs[open].status |= XYWS_MSG_INTERRUPTED;
+      m = (int64_t)nm++;
+      if ((uint64_t)m < msg_cap) {
+        memset(&msgs[m], 0, sizeof msgs[m]);
+        msgs[m].first_frame = i;
+        msgs[m].out_off = pos;
+        msgs[m].opcode = op;
+        msgs[m].status = orphans ? XYWS_MSG_ORPHANS : 0;
+      }
+      orphans = 0;
+      open = m;
+    } else {
+      if (open < 0) { orphans = 1; continue; }
+      m = open;
+    }
+    for (uint64_t j = 0; j < f->payload_len; j++, pos++) {
+      uint64_t sp = (uint64_t)f->payload_off + j;
+      if (pos < out_cap) out[pos] = sp < src_len ? src[sp] : 0;
+    }
+    if ((uint64_t)m < msg_cap) {
+      msgs[m].nframes++;
+      msgs[m].length += f->payload_len;
+    }
+    if (f->flags & XYWS_FLAG_FIN) {
+      if ((uint64_t)m < msg_cap) msgs[m].status |= XYWS_MSG_COMPLETE;
+      open = -1;
+    }
+  }
+  uint64_t lim = nm < msg_cap ? nm : msg_cap;
+  for (uint64_t m = 0; m < lim; m++) {
+    xyws_message* M = &msgs[m];
+    if (M->out_off + M->length > out_cap) M->status |= XYWS_MSG_TRUNCATED;
+    if ((opts & XYWS_REASM_UTF8) && M->opcode == XYWS_FLAG_OP_TEXT) {
+      uint64_t avail = M->out_off >= out_cap ? 0 : out_cap - M->out_off;
+      uint64_t len = M->length < avail ? M->length : avail;
+      int complete = (M->status & XYWS_MSG_COMPLETE) && !(M->status & XYWS_MSG_TRUNCATED);
+      if (!oracle_utf8_valid(out + M->out_off, len, complete)) M->status |= XYWS_MSG_UTF8_BAD;
+    }
+  }
+  return nm;
 }
 
 /* ---- synthetic batches + digest (shared spec: include/xyws_synth.h) ------ */

@@ -46,7 +46,7 @@ def test_struct_layouts_match_header():
 
 def test_abi_version_and_strerror():
     lib = L.load()
-    assert lib.xyws_abi_version() == 1
+    assert lib.xyws_abi_version() == 2
     assert lib.xyws_strerror(0) == b"ok"
     assert lib.xyws_strerror(-2) == b"HIP runtime error"
 

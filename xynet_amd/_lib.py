@@ -51,7 +51,27 @@ class Carry(C.Structure):
                 ("reserved", C.c_uint8 * 21)]
 
 
+class Verdict(C.Structure):
+    """xyws_verdict (include/xyws.h), 8 bytes."""
+    _fields_ = [("close_code", C.c_uint16), ("peer_code", C.c_uint16), ("action", C.c_uint8),
+                ("reserved", C.c_uint8 * 3)]
+
+
+class Message(C.Structure):
+    """xyws_message (include/xyws.h), 40 bytes."""
+    _fields_ = [("first_frame", C.c_uint64), ("nframes", C.c_uint64), ("out_off", C.c_uint64),
+                ("length", C.c_uint64), ("status", C.c_uint32), ("opcode", C.c_uint8),
+                ("reserved", C.c_uint8 * 3)]
+
+
 assert C.sizeof(Frame) == 32 and C.sizeof(Carry) == 64
+assert C.sizeof(Verdict) == 8 and C.sizeof(Message) == 40
+NPOS = (1 << 64) - 1
+ENC_FRAME_OPCODE = 0x1
+ACT_DATA, ACT_PING, ACT_PONG, ACT_CLOSE = 0, 1, 2, 3
+POL_FRAGMENTS, POL_UNMASKED, POL_STRICT = 0x1, 0x2, 0x4
+REASM_UTF8 = 0x1
+MSG_COMPLETE, MSG_UTF8_BAD, MSG_INTERRUPTED, MSG_TRUNCATED, MSG_ORPHANS = 0x1, 0x2, 0x4, 0x8, 0x10
 
 _lib = None
 _tools = None
@@ -101,6 +121,25 @@ def load():
     L.xyws_debug_records.argtypes = [vp, vp, C.POINTER(C.c_uint64), u64]
     L.xyws_decode_stream.restype = i32
     L.xyws_decode_stream.argtypes = [vp, vp, u64, vp, vp, vp, u64, vp, u32, vp]
+    # ABI 2
+    L.xyws_parser_create.restype = i32
+    L.xyws_parser_create.argtypes = [vp, C.POINTER(vp)]
+    L.xyws_parser_destroy.restype = i32
+    L.xyws_parser_destroy.argtypes = [vp]
+    L.xyws_parser_reset.restype = i32
+    L.xyws_parser_reset.argtypes = [vp]
+    L.xyws_parser_parse.restype = i32
+    L.xyws_parser_parse.argtypes = [vp, vp, u64, C.POINTER(u64), vp]
+    L.xyws_parser_result.restype = i32
+    L.xyws_parser_result.argtypes = [vp, C.POINTER(u8), vp, C.POINTER(u64)]
+    L.xyws_header_build.restype = u64
+    L.xyws_header_build.argtypes = [u8, vp, u64, vp]
+    L.xyws_encode_frames.restype = i32
+    L.xyws_encode_frames.argtypes = [vp, vp, u64, vp, u64, vp, u8, u32, vp, vp, u32, vp, u64, vp, vp, vp]
+    L.xyws_classify_frames.restype = i32
+    L.xyws_classify_frames.argtypes = [vp, vp, u64, vp, u64, vp, u64, u32, vp, vp, vp]
+    L.xyws_reassemble.restype = i32
+    L.xyws_reassemble.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp, u64, vp, u64, vp, vp]
     _lib = L
     return L
 

@@ -19,10 +19,10 @@ COMMON = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-W
           "-Wno-unused-function", "-I" + INC, "-I" + CSRC]
 
 TARGETS = {
-    "libxyws.so": ["xyws.hip", "xyws_stream.hip"],
+    "libxyws.so": ["xyws.hip", "xyws_stream.hip", "xyws_frames.hip"],
     "libxyws_tools.so": ["xyws_tools.hip"],
 }
-DEPS = ["xyws_device.h", "xyws_stream.h"]
+DEPS = ["xyws_device.h", "xyws_stream.h", "xyws_ctx.h"]
 
 
 def _stale(out, srcs):
@@ -48,7 +48,31 @@ def build(force=False, verbose=False, extra=None):
             raise RuntimeError(f"hipcc failed for {name}:\n{r.stdout}\n{r.stderr}")
         if verbose and r.stderr.strip():
             print(r.stderr)
+    build_cpp_tests(hipcc, force=force, verbose=verbose)
     return [os.path.join(PKG, n) for n in TARGETS]
+
+
+# C++ callers of the header-only shim (include/xyws/websocket.hpp), run by the
+# GPU tests: linked against the in-tree libxyws.so (rpath), built here so the
+# binary travels to the GPU box with the tree.
+CPP_TESTS = {"tests/cpp/test_shim": "tests/cpp/test_shim.cpp"}
+
+
+def build_cpp_tests(hipcc, force=False, verbose=False):
+    for out, src in CPP_TESTS.items():
+        out, src = os.path.join(ROOT, out), os.path.join(ROOT, src)
+        deps = [src, os.path.join(INC, "xyws.h"), os.path.join(INC, "xyws", "websocket.hpp"),
+                os.path.join(PKG, "libxyws.so")]
+        if not force and os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
+            continue
+        rpath = os.path.relpath(PKG, os.path.dirname(out))
+        cmd = [hipcc, "-std=c++20", "-O2", "-Wall", "-I" + INC, src, "-o", out, "-L" + PKG, "-lxyws",
+               "-Wl,-rpath,$ORIGIN/" + rpath]
+        if verbose:
+            print(" ".join(cmd))
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {out}:\n{r.stdout}\n{r.stderr}")
 
 
 if __name__ == "__main__":

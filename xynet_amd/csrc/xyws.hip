@@ -25,22 +25,11 @@
 #include "xyws.h"
 #include "xyws_device.h"
 #include "xyws_stream.h"
+#include "xyws_ctx.h"
 
 #ifndef XYWS_HAVE_FUSED
 #define XYWS_HAVE_FUSED 1
 #endif
-
-// ---------------------------------------------------------------------------
-// Frame table (device scratch, SoA) consumed by k_unmask_tiles. Entries are
-// sorted by position and non-overlapping; [ps, pe) is the payload range to
-// unmask (already clipped), kw the key word for 4-byte-aligned positions.
-struct frame_table {
-  uint64_t* start;
-  uint64_t* ps;
-  uint64_t* pe;
-  uint32_t* kw;
-  uint64_t* count;  // number of valid entries (device)
-};
 
 #define UNMASK_TILE 16384u
 #define UNMASK_THREADS 256u
@@ -274,111 +263,7 @@ __global__ void __launch_bounds__(UNMASK_THREADS) k_unmask_tiles(uint8_t* __rest
 // ===========================================================================
 // C-ABI
 // ===========================================================================
-// Device scratch is kept per (context, stream): a decode's run records, flags
-// and frame table belong to the stream it was enqueued on, so calls on one
-// context from several streams (an io_uring service overlapping batches) run
-// concurrently without sharing scratch. XYWS_SLOTS streams get a slot each;
-// when a further stream arrives while every slot is bound, the device is
-// synchronized (every slot idle) and the bindings start over.
-#define XYWS_SLOTS 16
-
-struct scratch_slot {
-  bool bound;
-  hipStream_t stream;
-  // frame table scratch (indexed + serial modes)
-  void* tab_mem;
-  uint64_t tab_cap;
-  stream_scratch ss;  // fused stream decoder scratch (xyws_stream.hip)
-};
-
-struct xyws_ctx {
-  int device;
-  std::mutex mu;
-  uint32_t* err;  // device error word (serial / indexed modes)
-  uint64_t reserve_bytes, reserve_frames;  // applied to every slot
-  scratch_slot slot[XYWS_SLOTS];
-};
-
-namespace {
-
-struct device_guard {
-  int prev = -1;
-  bool ok = false;
-  explicit device_guard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    ok = hipSetDevice(dev) == hipSuccess;
-  }
-  ~device_guard() {
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
-};
-
-int hip_err(hipError_t e) { return e == hipSuccess ? XYWS_OK : XYWS_ERR_HIP; }
-
-bool capturing(hipStream_t s) {
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  (void)hipStreamIsCapturing(s, &cs);
-  return cs != hipStreamCaptureStatusNone;
-}
-
-int ensure_table(scratch_slot* sl, uint64_t n, bool capture) {
-  if (n <= sl->tab_cap && sl->tab_mem) return XYWS_OK;
-  if (capture) return XYWS_ERR_CAPACITY;
-  uint64_t cap = n < 1024 ? 1024 : n;
-  void* mem = nullptr;
-  size_t bytes = cap * (8 + 8 + 8 + 4) + 64;
-  if (hipMalloc(&mem, bytes) != hipSuccess) return XYWS_ERR_NOMEM;
-  if (sl->tab_mem) {
-    (void)hipDeviceSynchronize();
-    (void)hipFree(sl->tab_mem);
-  }
-  sl->tab_mem = mem;
-  sl->tab_cap = cap;
-  return XYWS_OK;
-}
-
-frame_table table_of(scratch_slot* sl) {
-  frame_table t;
-  char* m = static_cast<char*>(sl->tab_mem);
-  t.start = reinterpret_cast<uint64_t*>(m);
-  t.ps = t.start + sl->tab_cap;
-  t.pe = t.ps + sl->tab_cap;
-  t.count = t.pe + sl->tab_cap;
-  t.kw = reinterpret_cast<uint32_t*>(t.count + 8);
-  return t;
-}
-
-int grid_for(uint64_t items, uint32_t per_block, uint32_t cap) {
-  uint64_t g = (items + per_block - 1) / per_block;
-  if (g < 1) g = 1;
-  if (g > cap) g = cap;
-  return (int)g;
-}
-
-// The slot of `stream` (ctx->mu held).
-int acquire_slot(xyws_ctx* ctx, hipStream_t stream, bool capture, scratch_slot** out) {
-  scratch_slot* pick = nullptr;
-  for (auto& sl : ctx->slot)
-    if (sl.bound && sl.stream == stream) { pick = &sl; break; }
-  if (!pick) {
-    bool any_free = false;
-    for (auto& sl : ctx->slot) any_free = any_free || !sl.bound;
-    if (!any_free) {
-      // every slot bound to another stream: wait until all of them are idle
-      if (capture) return XYWS_ERR_CAPACITY;
-      if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
-      for (auto& sl : ctx->slot) sl.bound = false;
-    }
-    for (auto& sl : ctx->slot)
-      if (!sl.bound) { pick = &sl; break; }
-  }
-  pick->bound = true;
-  pick->stream = stream;
-  *out = pick;
-  return XYWS_OK;
-}
-
-}  // namespace
+using namespace xyws_internal;
 
 extern "C" {
 
@@ -413,6 +298,8 @@ int xyws_ctx_create(int device, xyws_ctx** out) {
     sl.bound = false;
     sl.stream = nullptr;
     sl.tab_mem = nullptr;
+    sl.aux_mem = nullptr;
+    sl.aux_cap = 0;
     sl.tab_cap = 0;
     stream_scratch_init(&sl.ss, device);
   }
@@ -436,6 +323,7 @@ int xyws_ctx_destroy(xyws_ctx* ctx) {
     (void)hipDeviceSynchronize();
     for (auto& sl : ctx->slot) {
       if (sl.tab_mem) (void)hipFree(sl.tab_mem);
+      if (sl.aux_mem) (void)hipFree(sl.aux_mem);
       stream_scratch_free(&sl.ss);
     }
     if (ctx->err) (void)hipFree(ctx->err);
@@ -587,4 +475,112 @@ int xyws_decode_stream(xyws_ctx* ctx, void* dev_buf, uint64_t len, const xyws_ca
                              dev_nframes, opts, s);
 }
 
+// ---------------------------------------------------------------------------
+// websocket_frame_header_parser (websocket_frame_header.h:226-385) through the
+// device: each parse() hands the bytes that can still belong to the header
+// (at most 14 minus those already fed) to the stream decoder in parse-only
+// mode with the parser's device-resident carry, then reads back whether a
+// header completed. While no header has completed every byte fed so far is a
+// header byte, so the bytes consumed in the completing call are its hdr_len
+// minus the bytes fed before it (:342, :362, :375); once complete, parse()
+// returns npos until reset() (:378-384).
+struct xyws_parser {
+  xyws_ctx* ctx;
+  uint8_t* dev;       // device: carry (64 B) | frame (32 B) | count (8 B) | staging (32 B)
+  uint8_t* host;      // pinned: frame (32 B) | count (8 B)
+  uint64_t fed;       // header bytes fed since reset()
+  bool finished;
+  xyws_frame res;
+};
+
+int xyws_parser_create(xyws_ctx* ctx, xyws_parser** out) {
+  if (!ctx || !out) return XYWS_ERR_INVALID;
+  *out = nullptr;
+  device_guard g(ctx->device);
+  if (!g.ok) return XYWS_ERR_HIP;
+  xyws_parser* p = new xyws_parser();
+  p->ctx = ctx;
+  p->dev = nullptr;
+  p->host = nullptr;
+  if (hipMalloc(&p->dev, 256) != hipSuccess) {
+    delete p;
+    return XYWS_ERR_NOMEM;
+  }
+  if (hipHostMalloc(&p->host, 64, hipHostMallocDefault) != hipSuccess) {
+    (void)hipFree(p->dev);
+    delete p;
+    return XYWS_ERR_NOMEM;
+  }
+  *out = p;
+  return xyws_parser_reset(p);
+}
+
+int xyws_parser_destroy(xyws_parser* p) {
+  if (!p) return XYWS_ERR_INVALID;
+  device_guard g(p->ctx->device);
+  (void)hipDeviceSynchronize();
+  (void)hipFree(p->dev);
+  (void)hipHostFree(p->host);
+  delete p;
+  return XYWS_OK;
+}
+
+int xyws_parser_reset(xyws_parser* p) {
+  if (!p) return XYWS_ERR_INVALID;
+  device_guard g(p->ctx->device);
+  if (!g.ok) return XYWS_ERR_HIP;
+  p->fed = 0;
+  p->finished = false;
+  memset(&p->res, 0, sizeof p->res);
+  return hip_err(hipMemset(p->dev, 0, 64));  // a zero carry: a fresh parser (s_start)
+}
+
+int xyws_parser_parse(xyws_parser* p, const void* data, uint64_t len, uint64_t* consumed, void* stream) {
+  if (!p || !consumed || (!data && len)) return XYWS_ERR_INVALID;
+  *consumed = XYWS_NPOS;
+  if (p->finished || !len) return XYWS_OK;
+  device_guard g(p->ctx->device);
+  if (!g.ok) return XYWS_ERR_HIP;
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t room = XYWS_MAX_FRAME_HEADER_SIZE - p->fed;
+  const uint64_t n = len < room ? len : room;
+  xyws_carry* carry = reinterpret_cast<xyws_carry*>(p->dev);
+  xyws_frame* frame = reinterpret_cast<xyws_frame*>(p->dev + 64);
+  uint64_t* count = reinterpret_cast<uint64_t*>(p->dev + 96);
+  uint8_t* stage = p->dev + 128;
+  // device memory is parsed where it lies; host bytes are staged
+  const void* src = data;
+  hipPointerAttribute_t attr;
+  const bool on_dev = hipPointerGetAttributes(&attr, data) == hipSuccess && attr.type == hipMemoryTypeDevice;
+  (void)hipGetLastError();  // (an unregistered host pointer leaves an error behind)
+  if (!on_dev) {
+    if (hipMemcpyAsync(stage, data, n, hipMemcpyHostToDevice, s) != hipSuccess) return XYWS_ERR_HIP;
+    src = stage;
+  }
+  int rc = xyws_decode_stream(p->ctx, const_cast<void*>(src), n, carry, carry, frame, 1, count,
+                              XYWS_OPT_PARSE_ONLY, stream);
+  if (rc) return rc;
+  if (hipMemcpyAsync(p->host, frame, 40, hipMemcpyDeviceToHost, s) != hipSuccess) return XYWS_ERR_HIP;
+  if (hipStreamSynchronize(s) != hipSuccess) return XYWS_ERR_HIP;
+  uint64_t nf;
+  memcpy(&nf, p->host + 32, 8);
+  if (nf == 0) {
+    p->fed += n;
+    return XYWS_OK;
+  }
+  memcpy(&p->res, p->host, sizeof p->res);
+  p->finished = true;
+  *consumed = p->res.hdr_len - p->fed;
+  return XYWS_OK;
+}
+
+int xyws_parser_result(const xyws_parser* p, uint8_t* flags, uint8_t key[4], uint64_t* length) {
+  if (!p) return XYWS_ERR_INVALID;
+  if (flags) *flags = p->res.flags;
+  if (key) memcpy(key, p->res.key, 4);
+  if (length) *length = p->res.payload_len;
+  return XYWS_OK;
+}
+
 }  // extern "C"
+

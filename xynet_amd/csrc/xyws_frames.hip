@@ -1,0 +1,738 @@
+// xyws_frames.hip — gfx950 kernels over a decoded frame table (the callers
+// on either side of the decode path) and their C-ABI entry points:
+//
+//   xyws_encode_frames    batched detail::websocket_frame_header_builder
+//                         (include/xynet/http/websocket_frame_header.h:136-175)
+//                         + payload copy: echo_once's reply
+//                         (example/websocket/websocket_echo.cpp:18-27), or
+//                         client-role masked frames
+//   xyws_classify_frames  websocket_check_parser_result's close policy
+//                         (example/include/common/websocket.h:81-108)
+//   xyws_reassemble       FIN=0 chains gathered into messages + UTF-8 check
+//
+// All three are byte/integer work bound by HBM (the gathers) or by launch
+// latency (the per-frame passes): per-frame passes are one lane per frame;
+// frame-order offsets come from a three-kernel scan (block partials, one block
+// over the partials, fix-up); the gathers write 16 KiB output tiles per
+// workgroup, each lane four 16-byte chunks, with the items touching the tile
+// staged in LDS.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "xyws.h"
+#include "xyws_device.h"
+#include "xyws_ctx.h"
+
+using namespace xyws_internal;
+
+namespace {
+
+constexpr uint32_t FT = 256;           // threads per block, frame-list kernels
+constexpr uint32_t SB = 4 * FT;        // items per scan block (4 per lane)
+constexpr uint32_t GTILE = 16384;      // gather tile (bytes of output)
+constexpr uint32_t GLDS = 512;         // items staged per tile
+constexpr uint64_t U64MAX = ~0ull;
+
+// ---------------------------------------------------------------- header build
+// detail::websocket_frame_header_builder (:136-175) into four little-endian
+// words (byte i = w[i/4] >> 8*(i%4)); returns H. The key word kw (wire bytes,
+// little-endian) is written only when has_key, as the builder copies the
+// key only for a non-null mask (:168-173). Register-only (no byte array).
+__host__ __device__ inline uint32_t build_header(uint32_t flags, uint64_t len, bool has_key, uint32_t kw,
+                                                 uint32_t w[4]) {
+  const uint32_t b0 = ((flags & XYWS_FLAG_FIN) ? 0x80u : 0u) | (flags & XYWS_FLAG_OP_MASK);
+  uint32_t b1 = (flags & XYWS_FLAG_HAS_MASK) ? 0x80u : 0u;
+  const bool masked = (flags & XYWS_FLAG_HAS_MASK) != 0;
+  const uint32_t k = has_key ? kw : 0u;
+  w[0] = w[1] = w[2] = w[3] = 0;
+  uint32_t h;
+  if (len < 126u) {
+    b1 |= (uint32_t)len;
+    w[0] = b0 | (b1 << 8);
+    if (masked) { w[0] |= k << 16; w[1] = k >> 16; }
+    h = 2;
+  } else if (len <= 0xFFFFu) {
+    b1 |= 126u;
+    w[0] = b0 | (b1 << 8) | ((uint32_t)(len >> 8) << 16) | ((uint32_t)(len & 0xFFu) << 24);
+    if (masked) w[1] = k;
+    h = 4;
+  } else {
+    b1 |= 127u;
+    // bytes 2..9: the length big-endian = the little-endian bytes of bswap64(len)
+    uint64_t be = 0;
+    for (int i = 0; i < 8; i++) be |= ((len >> (8 * i)) & 0xFFull) << (56 - 8 * i);
+    w[0] = b0 | (b1 << 8) | ((uint32_t)(be & 0xFFFFu) << 16);
+    w[1] = (uint32_t)(be >> 16);
+    w[2] = (uint32_t)(be >> 48);
+    if (masked) { w[2] |= k << 16; w[3] = k >> 16; }
+    h = 10;
+  }
+  return masked ? h + 4 : h;
+}
+
+XYWS_DEV uint64_t n_eff(uint64_t n, const uint64_t* dev_n) {
+  if (!dev_n) return n;
+  const uint64_t m = *dev_n;
+  return m < n ? m : n;
+}
+
+// ---------------------------------------------------------------- scans
+// Inclusive/exclusive scans of n u64 values in three kernels: block partials,
+// one block over the partials, fix-up. Rev scans from the end (index n-1-i).
+struct op_sum {
+  static XYWS_DEV uint64_t id() { return 0; }
+  static XYWS_DEV uint64_t f(uint64_t a, uint64_t b) { return a + b; }
+};
+struct op_max {
+  static XYWS_DEV uint64_t id() { return 0; }
+  static XYWS_DEV uint64_t f(uint64_t a, uint64_t b) { return a > b ? a : b; }
+};
+struct op_min {
+  static XYWS_DEV uint64_t id() { return U64MAX; }
+  static XYWS_DEV uint64_t f(uint64_t a, uint64_t b) { return a < b ? a : b; }
+};
+
+// Block-wide scan of one value per lane (FT lanes): *exc / return = the
+// lane's exclusive / inclusive prefix, *tot the block total.
+template <class Op>
+XYWS_DEV uint64_t block_scan(uint64_t v, uint64_t* sh, uint64_t* exc, uint64_t* tot) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x = Op::f(y, x);
+  }
+  uint64_t xe = __shfl_up(x, 1, 64);
+  if (lane == 63) sh[wave] = x;
+  __syncthreads();
+  uint64_t pre = Op::id(), all = Op::id();
+  for (uint32_t w = 0; w < FT / 64; w++) {
+    if (w < wave) pre = Op::f(pre, sh[w]);
+    all = Op::f(all, sh[w]);
+  }
+  __syncthreads();
+  *tot = all;
+  *exc = lane ? Op::f(pre, xe) : pre;
+  return Op::f(pre, x);
+}
+
+template <class Op, bool Rev>
+XYWS_DEV uint64_t at(uint64_t n, uint64_t i) { return Rev ? n - 1 - i : i; }
+
+// pass 1: x[idx] <- the block-local scan (exclusive if Excl); part[b] <- total
+template <class Op, bool Rev, bool Excl>
+__global__ void __launch_bounds__(FT) k_scan_local(uint64_t* x, uint64_t n, uint64_t* part) {
+  __shared__ uint64_t sh[FT / 64];
+  const uint64_t i0 = (uint64_t)blockIdx.x * SB + 4ull * threadIdx.x;
+  uint64_t v[4], acc = Op::id();
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    v[k] = i0 + k < n ? x[at<Op, Rev>(n, i0 + k)] : Op::id();
+    acc = Op::f(acc, v[k]);
+  }
+  uint64_t run, tot;
+  (void)block_scan<Op>(acc, sh, &run, &tot);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint64_t out = Excl ? run : Op::f(run, v[k]);
+    run = Op::f(run, v[k]);
+    if (i0 + k < n) x[at<Op, Rev>(n, i0 + k)] = out;
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+// pass 2: one block scans the nb partials exclusively in place; *total <- all
+template <class Op>
+__global__ void __launch_bounds__(FT) k_scan_parts(uint64_t* part, uint64_t nb, uint64_t* total) {
+  __shared__ uint64_t sh[FT / 64];
+  uint64_t carry = Op::id();
+  for (uint64_t c = 0; c < nb; c += FT) {
+    const uint64_t i = c + threadIdx.x;
+    const uint64_t v = i < nb ? part[i] : Op::id();
+    uint64_t ex, tot;
+    (void)block_scan<Op>(v, sh, &ex, &tot);
+    if (i < nb) part[i] = Op::f(carry, ex);
+    carry = Op::f(carry, tot);
+  }
+  if (threadIdx.x == 0 && total) *total = carry;
+}
+
+// pass 3: x[idx] <- part[block] (op) x[idx]; exclusive scans also x[n] <- total
+template <class Op, bool Rev, bool Excl>
+__global__ void __launch_bounds__(FT) k_scan_fix(uint64_t* x, uint64_t n, const uint64_t* part,
+                                                  const uint64_t* total) {
+  const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
+  if (Excl && i == 0 && total) x[n] = *total;
+  if (i >= n) return;
+  const uint64_t p = part[i / SB];
+  const uint64_t j = at<Op, Rev>(n, i);
+  x[j] = Op::f(p, x[j]);
+}
+
+// Scan n values in place (device memory x, n+1 words when Excl && total),
+// part: (n / SB + 1) words of scratch, total: device word (nullable).
+template <class Op, bool Rev, bool Excl>
+int scan(uint64_t* x, uint64_t n, uint64_t* part, uint64_t* total, hipStream_t s) {
+  const uint64_t nb = (n + SB - 1) / SB;
+  if (nb == 0) {
+    if (Excl && total) {
+      hipLaunchKernelGGL((k_scan_parts<Op>), dim3(1), dim3(FT), 0, s, part, 0ull, total);
+      hipLaunchKernelGGL((k_scan_fix<Op, Rev, Excl>), dim3(1), dim3(FT), 0, s, x, 0ull, part, total);
+    }
+    return hip_err(hipGetLastError());
+  }
+  hipLaunchKernelGGL((k_scan_local<Op, Rev, Excl>), dim3(nb), dim3(FT), 0, s, x, n, part);
+  hipLaunchKernelGGL((k_scan_parts<Op>), dim3(1), dim3(FT), 0, s, part, nb, total);
+  hipLaunchKernelGGL((k_scan_fix<Op, Rev, Excl>), dim3((n + FT - 1) / FT), dim3(FT), 0, s, x, n,
+                     (const uint64_t*)part, (const uint64_t*)total);
+  return hip_err(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- gather
+// One item of a gather: output [dst, dst + H + len) = header bytes hw (H of
+// them) then src[soff .. soff + len) XOR the key (payload index from 0).
+struct gitem {
+  uint64_t dst, soff, len;
+  uint32_t hw[4];
+  uint32_t h, key;
+};
+
+enum { G_ENC = 0, G_REASM = 1 };
+
+struct gparams {
+  const uint8_t* src;  // 16-byte aligned base; the frame table's offset p is src[src_lo + p]
+  uint64_t src_lo, src_len;
+  const xyws_frame* frames;
+  const uint64_t* off;  // n_eff + 1 exclusive offsets of the items' outputs
+  uint64_t n;
+  const uint64_t* dev_n;
+  uint32_t mode, flags, enc_opts;
+  const uint8_t* keys;
+  uint8_t* out;  // 16-byte aligned base; output byte q lives at out[out_lo + q]
+  uint64_t out_lo, out_cap;
+  uint32_t* err;
+};
+
+XYWS_DEV uint32_t reply_flags(const gparams& G, uint32_t fflags) {
+  if (!(G.enc_opts & XYWS_ENC_FRAME_OPCODE)) return G.flags;
+  uint32_t op = fflags & XYWS_FLAG_OP_MASK;
+  if (op == XYWS_FLAG_OP_PING) op = XYWS_FLAG_OP_PONG;
+  return op | (fflags & XYWS_FLAG_FIN) | (G.flags & XYWS_FLAG_HAS_MASK);
+}
+
+XYWS_DEV gitem item_of(const gparams& G, uint64_t i) {
+  gitem it;
+  const xyws_frame f = G.frames[i];
+  it.dst = G.off[i];
+  const uint64_t size = G.off[i + 1] - it.dst;
+  it.soff = (uint64_t)f.payload_off;
+  it.hw[0] = it.hw[1] = it.hw[2] = it.hw[3] = 0;
+  it.h = 0;
+  it.key = 0;
+  if (G.mode == G_ENC && size) {
+    const uint32_t fl = reply_flags(G, f.flags);
+    uint32_t kw = 0;
+    const bool have = G.keys && (fl & XYWS_FLAG_HAS_MASK);
+    if (have)
+      kw = (uint32_t)G.keys[4 * i] | ((uint32_t)G.keys[4 * i + 1] << 8) | ((uint32_t)G.keys[4 * i + 2] << 16) |
+           ((uint32_t)G.keys[4 * i + 3] << 24);
+    it.h = build_header(fl, f.payload_len, have, kw, it.hw);
+    it.key = kw;
+  }
+  it.len = size - it.h;
+  return it;
+}
+
+XYWS_DEV uint8_t src_byte(const gparams& G, uint64_t p) {
+  if (p < G.src_len) return G.src[G.src_lo + p];
+  atomicOr(G.err, 0x100u);
+  return 0;
+}
+
+// Byte q (output coordinate) of item `it`.
+XYWS_DEV uint8_t item_byte(const gparams& G, const gitem& it, uint64_t q) {
+  const uint64_t r = q - it.dst;
+  if (r < it.h) return (uint8_t)(it.hw[r >> 2] >> (8u * (r & 3u)));
+  const uint64_t j = r - it.h;
+  return src_byte(G, it.soff + j) ^ (uint8_t)(it.key >> (8u * (j & 3u)));
+}
+
+// 16 source bytes from byte position p (any alignment; p + 16 <= src_len),
+// as four little-endian words: two aligned 16-byte loads and a funnel shift.
+XYWS_DEV void load16(const uint8_t* src, uint64_t p, uint32_t w[4]) {
+  const uint64_t a = p & ~15ull;
+  const u32x4 x = *reinterpret_cast<const u32x4*>(src + a);
+  const uint32_t sh = (uint32_t)(p & 15u);
+  if (!sh) {
+    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+    return;
+  }
+  const u32x4 y = *reinterpret_cast<const u32x4*>(src + a + 16);
+  const uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+  const uint32_t d = sh >> 2, b = sh & 3u;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t lo = v[0], hi = v[1];
+    // (select instead of a dynamic index into v: no scratch)
+#pragma unroll
+    for (uint32_t s = 1; s < 4; s++)
+      if (d == s) { lo = v[s + k]; hi = v[s + k + 1]; }
+    if (d == 0) { lo = v[k]; hi = v[k + 1]; }
+    w[k] = b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
+  }
+}
+
+// The last item whose output starts at or before q, among items [a, b) whose
+// starts (off) are ascending; from LDS (ls != null) or memory.
+XYWS_DEV uint64_t find_item(const uint64_t* ls, const uint64_t* off, uint64_t a, uint64_t b, uint64_t base,
+                            uint64_t q) {
+  // invariant: start(a) <= q, answer in [a, b)
+  uint64_t lo = a, hi = b;
+  while (hi - lo > 1) {
+    const uint64_t m = (lo + hi) >> 1;
+    const uint64_t v = ls ? ls[m - base] : off[m];
+    if (v <= q) lo = m; else hi = m;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(FT) k_gather(gparams G) {
+  __shared__ uint64_t s_off[GLDS + 1];
+  __shared__ uint64_t s_f0, s_f1;
+  const uint64_t ne = n_eff(G.n, G.dev_n);
+  const uint64_t total = G.off[ne];
+  const uint64_t lim = total < G.out_cap ? total : G.out_cap;  // bytes written
+  if (!lim || !ne) return;
+  // output chunks are 16-byte aligned in the out[] coordinate: q in [0, lim)
+  // sits at out_lo + q
+  const uint64_t o0 = G.out_lo, o1 = G.out_lo + lim;
+  const uint64_t ntiles = (o1 + GTILE - 1) / GTILE;
+  for (uint64_t tile = blockIdx.x + (o0 / GTILE); tile < ntiles; tile += gridDim.x) {
+    const uint64_t t0 = tile * GTILE, t1 = t0 + GTILE;
+    const uint64_t q0 = t0 > o0 ? t0 - o0 : 0, q1 = (t1 < o1 ? t1 : o1) - o0;  // output range of the tile
+    if (threadIdx.x == 0) {
+      s_f0 = find_item(nullptr, G.off, 0, ne, 0, q0);
+      s_f1 = find_item(nullptr, G.off, 0, ne, 0, q1 - 1) + 1;  // items [f0, f1) touch the tile
+    }
+    __syncthreads();
+    const uint64_t f0 = s_f0, f1 = s_f1;
+    const bool in_lds = f1 - f0 <= GLDS;
+    if (in_lds)
+      for (uint64_t k = threadIdx.x; k <= f1 - f0; k += FT) s_off[k] = G.off[f0 + k];
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t c = 0; c < GTILE / 16 / FT; c++) {
+      const uint64_t a = t0 + (uint64_t)(c * FT + threadIdx.x) * 16;  // aligned out[] position
+      if (a + 16 <= o0 || a >= o1) continue;
+      const uint64_t qa = a > o0 ? a - o0 : 0;  // first output byte of the chunk
+      const uint64_t g = find_item(in_lds ? s_off : nullptr, G.off, f0, f1, f0, qa);
+      gitem it = item_of(G, g);
+      const uint64_t ps = it.dst + it.h, pe = ps + it.len;  // payload part of the item
+      uint32_t w[4];
+      if (a >= o0 && a + 16 <= o1 && a - o0 >= ps && a - o0 + 16 <= pe &&
+          it.soff + (a - o0 - ps) + 16 <= G.src_len) {
+        // the whole chunk is payload of one item: 16 source bytes
+        const uint64_t j = a - o0 - ps;
+        load16(G.src, G.src_lo + it.soff + j, w);
+        const uint32_t kw = rotr8(it.key, (uint32_t)j);
+        w[0] ^= kw; w[1] ^= kw; w[2] ^= kw; w[3] ^= kw;
+        *reinterpret_cast<u32x4*>(G.out + a) = u32x4{w[0], w[1], w[2], w[3]};
+      } else {
+        // headers, item boundaries, edges: byte by byte
+        uint64_t gi = g;
+        uint64_t nxt = gi + 1 < ne ? (in_lds && gi + 1 - f0 <= GLDS ? s_off[gi + 1 - f0] : G.off[gi + 1]) : U64MAX;
+        for (uint32_t t = 0; t < 16; t++) {
+          const uint64_t p = a + t;
+          if (p < o0 || p >= o1) continue;
+          const uint64_t q = p - o0;
+          while (q >= nxt) {
+            gi++;
+            it = item_of(G, gi);
+            nxt = gi + 1 < ne ? G.off[gi + 1] : U64MAX;
+          }
+          G.out[p] = item_byte(G, it, q);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- encode
+// sizes: header + payload of every selected frame (0 for the others)
+__global__ void __launch_bounds__(FT) k_enc_sizes(gparams G, const xyws_verdict* verd, uint32_t amask,
+                                                  uint64_t* sz) {
+  const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
+  if (i >= G.n) return;
+  const uint64_t ne = n_eff(G.n, G.dev_n);
+  uint64_t s = 0;
+  if (i < ne && (!verd || (amask >> verd[i].action) & 1u)) {
+    const xyws_frame f = G.frames[i];
+    uint32_t w[4];
+    s = build_header(reply_flags(G, f.flags), f.payload_len, false, 0, w) + f.payload_len;
+  }
+  sz[i] = s;
+}
+
+// ---------------------------------------------------------------- classify
+__global__ void __launch_bounds__(FT) k_classify(const uint8_t* src, uint64_t src_len, const xyws_frame* frames,
+                                                 uint64_t n, const uint64_t* dev_n, uint64_t max_payload,
+                                                 uint32_t policy, xyws_verdict* out, uint64_t* first) {
+  const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
+  const uint64_t ne = n_eff(n, dev_n);
+  if (i >= ne) return;
+  const xyws_frame f = frames[i];
+  const uint32_t op = f.flags & XYWS_FLAG_OP_MASK;
+  xyws_verdict v;
+  v.close_code = 0;
+  v.peer_code = 0;
+  v.action = op == XYWS_FLAG_OP_PING ? XYWS_ACT_PING : op == XYWS_FLAG_OP_PONG ? XYWS_ACT_PONG : XYWS_ACT_DATA;
+  v.reserved[0] = v.reserved[1] = v.reserved[2] = 0;
+  const bool proto = (f.status & (XYWS_ST_RSV | XYWS_ST_RESERVED_OPCODE | XYWS_ST_BAD_CONTROL)) != 0;
+  uint16_t code = 0;
+  if ((policy & XYWS_POL_STRICT) && proto) code = 1002;
+  else if (op == XYWS_FLAG_OP_CLOSE) code = 1000;  // (websocket.h:87-90, opcode compared exactly)
+  else if (!(f.flags & XYWS_FLAG_FIN) && !(policy & XYWS_POL_FRAGMENTS)) code = 1003;
+  else if (!(f.flags & XYWS_FLAG_HAS_MASK) && !(policy & XYWS_POL_UNMASKED)) code = 1008;
+  else if (f.payload_len > max_payload) code = 1009;
+  if (op == XYWS_FLAG_OP_CLOSE) {
+    v.action = XYWS_ACT_CLOSE;
+    const uint64_t p = (uint64_t)f.payload_off;
+    v.peer_code = 1005;  // (RFC 6455 7.4.1: no status code present)
+    if (f.payload_len >= 2 && p + 2 <= src_len) v.peer_code = (uint16_t)((src[p] << 8) | src[p + 1]);
+  }
+  if (code) {
+    v.close_code = code;
+    v.action = XYWS_ACT_CLOSE;
+    if (first) atomicMin(reinterpret_cast<unsigned long long*>(first), (unsigned long long)i);
+  }
+  out[i] = v;
+}
+
+// ---------------------------------------------------------------- reassembly
+// a[i] = 1 + i for a text/binary frame (a message start), else 0; b[i] = i
+// for a data frame with FIN, else UINT64_MAX; st[i] = 1 for a start
+__global__ void __launch_bounds__(FT) k_rs_marks(const xyws_frame* frames, uint64_t n, const uint64_t* dev_n,
+                                                 uint64_t* a, uint64_t* b, uint64_t* st) {
+  const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t ne = n_eff(n, dev_n);
+  uint64_t va = 0, vb = U64MAX, vs = 0;
+  if (i < ne) {
+    const uint32_t fl = frames[i].flags, op = fl & XYWS_FLAG_OP_MASK;
+    const bool start = op == XYWS_FLAG_OP_TEXT || op == XYWS_FLAG_OP_BINARY;
+    if (start) { va = i + 1; vs = 1; }
+    if (op <= XYWS_FLAG_OP_BINARY && (fl & XYWS_FLAG_FIN)) vb = i;
+  }
+  a[i] = va;
+  b[i] = vb;
+  st[i] = vs;
+}
+
+// After the scans: a[i] = 1 + the last start <= i (0: none), b[i] = the next
+// data frame with FIN >= i. Frame i belongs to the message of s = a[i] - 1
+// when it is a data frame and i <= b[s]. sz[i] = its payload bytes, cnt[i] =
+// 1 for members; orphan continuations raise orph[the next start's rank].
+__global__ void __launch_bounds__(FT) k_rs_sizes(const xyws_frame* frames, uint64_t n, const uint64_t* dev_n,
+                                                 const uint64_t* a, const uint64_t* b, uint64_t* sz,
+                                                 uint64_t* cnt, uint64_t* orphan_flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t ne = n_eff(n, dev_n);
+  uint64_t s = 0, c = 0;
+  if (i < ne) {
+    const xyws_frame f = frames[i];
+    const uint32_t op = f.flags & XYWS_FLAG_OP_MASK;
+    if (op <= XYWS_FLAG_OP_BINARY) {
+      const uint64_t st = a[i];
+      if (st && i <= b[st - 1]) {
+        s = f.payload_len;
+        c = 1;
+      } else {
+        orphan_flag[i] = 1;  // (a continuation outside a message: dropped)
+      }
+    }
+  }
+  sz[i] = s;
+  cnt[i] = c;
+}
+
+// message records: first_frame by rank (st[] exclusive-scanned = ranks)
+__global__ void __launch_bounds__(FT) k_rs_first(const xyws_frame* frames, uint64_t n, const uint64_t* dev_n,
+                                                 const uint64_t* rank, xyws_message* msgs, uint64_t msg_cap) {
+  const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
+  const uint64_t ne = n_eff(n, dev_n);
+  if (i >= ne) return;
+  const uint32_t op = frames[i].flags & XYWS_FLAG_OP_MASK;
+  if (op != XYWS_FLAG_OP_TEXT && op != XYWS_FLAG_OP_BINARY) return;
+  const uint64_t m = rank[i];
+  if (m < msg_cap) {
+    msgs[m].first_frame = i;
+    msgs[m].opcode = (uint8_t)op;
+  }
+}
+
+// the rest of each record from the offsets of its start and the next start
+__global__ void __launch_bounds__(FT) k_rs_msgs(const uint64_t* dev_n, uint64_t n, const uint64_t* nmsg_p,
+                                                const uint64_t* off, const uint64_t* cntoff, const uint64_t* b,
+                                                const uint64_t* orphan, const uint64_t* orph_rank,
+                                                uint64_t out_cap, xyws_message* msgs, uint64_t msg_cap,
+                                                uint64_t* dev_nmsgs) {
+  const uint64_t m = (uint64_t)blockIdx.x * FT + threadIdx.x;
+  const uint64_t ne = n_eff(n, dev_n), nm = *nmsg_p;
+  if (m == 0 && dev_nmsgs) *dev_nmsgs = nm;
+  if (m >= nm || m >= msg_cap) return;
+  const uint64_t s = msgs[m].first_frame;
+  const uint64_t ns = m + 1 < nm && m + 1 < msg_cap ? msgs[m + 1].first_frame : ne;
+  msgs[m].out_off = off[s];
+  msgs[m].length = off[ns] - off[s];
+  msgs[m].nframes = cntoff[ns] - cntoff[s];
+  uint32_t st = 0;
+  if (b[s] < ns) st |= XYWS_MSG_COMPLETE;
+  else if (m + 1 < nm) st |= XYWS_MSG_INTERRUPTED;
+  if (off[ns] > out_cap) st |= XYWS_MSG_TRUNCATED;
+  // orphans between the previous start (or the batch start) and this one:
+  // orph_rank = orphan flags prefix-summed; orphans before s minus those
+  // before the previous start
+  const uint64_t ps = m ? msgs[m - 1].first_frame : 0;
+  if (orph_rank[s] - (m ? orph_rank[ps] : 0) > 0) st |= XYWS_MSG_ORPHANS;
+  (void)orphan;
+  msgs[m].status = st;
+  msgs[m].reserved[0] = msgs[m].reserved[1] = msgs[m].reserved[2] = 0;
+}
+
+// UTF-8 (RFC 3629) over every text message's bytes in out[out_lo + ...]; one
+// lane per 16-byte chunk, neighbours read for sequences crossing chunks.
+XYWS_DEV uint32_t lead_len(uint32_t c) { return c >= 0xF0u ? 4u : c >= 0xE0u ? 3u : c >= 0xC0u ? 2u : 0u; }
+
+__global__ void __launch_bounds__(FT) k_utf8(const uint8_t* out, uint64_t out_lo, uint64_t out_cap,
+                                             const uint64_t* nmsg_p, xyws_message* msgs, uint64_t msg_cap) {
+  const uint64_t nm0 = *nmsg_p, nm = nm0 < msg_cap ? nm0 : msg_cap;
+  if (!nm) return;
+  const uint64_t total0 = msgs[nm - 1].out_off + msgs[nm - 1].length;
+  const uint64_t total = total0 < out_cap ? total0 : out_cap;
+  const uint64_t nch = (total + 15) / 16;
+  for (uint64_t ch = (uint64_t)blockIdx.x * FT + threadIdx.x; ch < nch; ch += (uint64_t)gridDim.x * FT) {
+    const uint64_t q0 = ch * 16;
+    // the last message starting at or before q0
+    uint64_t lo = 0, hi = nm;
+    while (hi - lo > 1) {
+      const uint64_t md = (lo + hi) >> 1;
+      if (msgs[md].out_off <= q0) lo = md; else hi = md;
+    }
+    uint64_t m = lo;
+    for (uint32_t t = 0; t < 16; t++) {
+      const uint64_t q = q0 + t;
+      if (q >= total) break;
+      while (m + 1 < nm && msgs[m + 1].out_off <= q) m++;
+      const uint64_t mo = msgs[m].out_off, me = mo + msgs[m].length;
+      if (msgs[m].opcode != XYWS_FLAG_OP_TEXT || q < mo || q >= me) continue;
+      const uint32_t mst = msgs[m].status;
+      const uint32_t c = out[out_lo + q];
+      bool bad = false;
+      if (c < 0x80u) {
+      } else if (c < 0xC0u) {
+        // a continuation byte: a lead within 3 bytes before must claim it
+        bool claimed = false;
+        for (uint32_t d = 1; d <= 3 && !claimed; d++) {
+          if (q < mo + d) break;
+          if (lead_len(out[out_lo + q - d]) > d) claimed = true;
+        }
+        bad = !claimed;
+      } else if (c == 0xC0u || c == 0xC1u || c >= 0xF5u) {
+        bad = true;
+      } else {
+        const uint32_t L = lead_len(c);
+        if (q + L > me || q + L > total) {
+          // cut by the end: invalid only in a complete message whose bytes
+          // all fit (an incomplete message continues in a later batch)
+          bad = (mst & XYWS_MSG_COMPLETE) && !(mst & XYWS_MSG_TRUNCATED);
+        } else {
+          for (uint32_t d = 1; d < L; d++)
+            if ((out[out_lo + q + d] & 0xC0u) != 0x80u) bad = true;
+          const uint32_t c1 = out[out_lo + q + 1];
+          if (c == 0xE0u && c1 < 0xA0u) bad = true;  // overlong
+          if (c == 0xEDu && c1 > 0x9Fu) bad = true;  // surrogates
+          if (c == 0xF0u && c1 < 0x90u) bad = true;  // overlong
+          if (c == 0xF4u && c1 > 0x8Fu) bad = true;  // above U+10FFFF
+        }
+      }
+      if (bad) atomicOr(&msgs[m].status, XYWS_MSG_UTF8_BAD);
+    }
+  }
+}
+
+__global__ void k_put(uint64_t* p, uint64_t v) { *p = v; }
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+uint64_t xyws_header_build(uint8_t flags, const uint8_t* key, uint64_t len, uint8_t out[14]) {
+  uint32_t w[4];
+  const uint32_t kw = key ? ((uint32_t)key[0] | ((uint32_t)key[1] << 8) | ((uint32_t)key[2] << 16) |
+                             ((uint32_t)key[3] << 24))
+                          : 0u;
+  const uint32_t h = build_header(flags, len, key != nullptr, kw, w);
+  if (out)
+    for (uint32_t i = 0; i < h; i++) out[i] = (uint8_t)(w[i >> 2] >> (8u * (i & 3u)));
+  return h;
+}
+
+int xyws_encode_frames(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, const xyws_frame* dev_frames,
+                       uint64_t n, const uint64_t* dev_n, uint8_t flags, uint32_t enc_opts,
+                       const uint8_t* dev_keys, const xyws_verdict* dev_verdicts, uint32_t action_mask,
+                       void* dev_out, uint64_t out_cap, uint64_t* dev_offsets, uint64_t* dev_out_len,
+                       void* stream) {
+  if (!ctx || (!dev_frames && n) || (!dev_src && src_len) || (!dev_out && out_cap)) return XYWS_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  device_guard gd(ctx->device);
+  if (!gd.ok) return XYWS_ERR_HIP;
+  hipStream_t s = (hipStream_t)stream;
+  const bool capt = capturing(s);
+  scratch_slot* sl = nullptr;
+  int rc = acquire_slot(ctx, s, capt, &sl);
+  if (rc) return rc;
+  // scratch: offsets (n + 1, unless the caller's), block partials, total
+  const uint64_t nb = (n + SB - 1) / SB + 1;
+  if ((rc = ensure_aux(sl, 8 * ((dev_offsets ? 0 : n + 1) + nb + 2), capt))) return rc;
+  uint64_t* aux = static_cast<uint64_t*>(sl->aux_mem);
+  uint64_t* off = dev_offsets ? dev_offsets : aux;
+  uint64_t* part = dev_offsets ? aux : aux + n + 1;
+  uint64_t* total = part + nb;
+  const uintptr_t oa = reinterpret_cast<uintptr_t>(dev_out);
+  const uintptr_t sa = reinterpret_cast<uintptr_t>(dev_src);
+  gparams G;
+  G.src = reinterpret_cast<const uint8_t*>(sa & ~(uintptr_t)15);
+  G.src_lo = sa & 15;
+  G.src_len = src_len;
+  G.frames = dev_frames;
+  G.off = off;
+  G.n = n;
+  G.dev_n = dev_n;
+  G.mode = G_ENC;
+  G.flags = flags;
+  G.enc_opts = enc_opts;
+  G.keys = dev_keys;
+  G.out = reinterpret_cast<uint8_t*>(oa & ~(uintptr_t)15);
+  G.out_lo = oa & 15;
+  G.out_cap = out_cap;
+  G.err = ctx->err;
+  if (n) {
+    hipLaunchKernelGGL(k_enc_sizes, dim3((n + FT - 1) / FT), dim3(FT), 0, s, G, dev_verdicts, action_mask, off);
+    if ((rc = hip_err(hipGetLastError()))) return rc;
+  }
+  if ((rc = scan<op_sum, false, true>(off, n, part, total, s))) return rc;
+  if (dev_out_len) {
+    if ((rc = hip_err(hipMemcpyAsync(dev_out_len, total, 8, hipMemcpyDeviceToDevice, s)))) return rc;
+  }
+  if (n && out_cap) {
+    const uint64_t tiles = (G.out_lo + out_cap + GTILE - 1) / GTILE;
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(tiles, 1, 8192)), dim3(FT), 0, s, G);
+    if ((rc = hip_err(hipGetLastError()))) return rc;
+  }
+  return XYWS_OK;
+}
+
+int xyws_classify_frames(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, const xyws_frame* dev_frames,
+                         uint64_t n, const uint64_t* dev_n, uint64_t max_payload, uint32_t policy,
+                         xyws_verdict* dev_verdicts, uint64_t* dev_first_close, void* stream) {
+  if (!ctx || (!dev_frames && n) || (!dev_verdicts && n)) return XYWS_ERR_INVALID;
+  device_guard gd(ctx->device);
+  if (!gd.ok) return XYWS_ERR_HIP;
+  hipStream_t s = (hipStream_t)stream;
+  if (dev_first_close) {
+    hipLaunchKernelGGL(k_put, dim3(1), dim3(1), 0, s, dev_first_close, U64MAX);
+  }
+  if (n) {
+    hipLaunchKernelGGL(k_classify, dim3((n + FT - 1) / FT), dim3(FT), 0, s,
+                       static_cast<const uint8_t*>(dev_src), src_len, dev_frames, n, dev_n, max_payload, policy,
+                       dev_verdicts, dev_first_close);
+  }
+  return hip_err(hipGetLastError());
+}
+
+int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, const xyws_frame* dev_frames,
+                    uint64_t n, const uint64_t* dev_n, uint32_t opts, void* dev_out, uint64_t out_cap,
+                    xyws_message* dev_msgs, uint64_t msg_cap, uint64_t* dev_nmsgs, void* stream) {
+  if (!ctx || (!dev_frames && n) || (!dev_src && src_len) || (!dev_out && out_cap) || (!dev_msgs && msg_cap))
+    return XYWS_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  device_guard gd(ctx->device);
+  if (!gd.ok) return XYWS_ERR_HIP;
+  hipStream_t s = (hipStream_t)stream;
+  const bool capt = capturing(s);
+  scratch_slot* sl = nullptr;
+  int rc = acquire_slot(ctx, s, capt, &sl);
+  if (rc) return rc;
+  // scratch: a, b, st/rank, sz/off, cnt/cntoff, orphan flags/prefix (n + 1
+  // each), block partials, totals
+  const uint64_t w = n + 1, nb = (n + SB - 1) / SB + 1;
+  if ((rc = ensure_aux(sl, 8 * (6 * w + nb + 4), capt))) return rc;
+  uint64_t* A = static_cast<uint64_t*>(sl->aux_mem);
+  uint64_t *a = A, *b = A + w, *st = A + 2 * w, *off = A + 3 * w, *cnt = A + 4 * w, *orph = A + 5 * w;
+  uint64_t* part = A + 6 * w;
+  uint64_t* tot = part + nb;  // tot[0]: bytes, tot[1]: messages, tot[2], tot[3]: scratch totals
+  if ((rc = hip_err(hipMemsetAsync(orph, 0, 8 * w, s)))) return rc;
+  const dim3 gn((uint32_t)((n + FT - 1) / FT > 0 ? (n + FT - 1) / FT : 1));
+  if (n) {
+    hipLaunchKernelGGL(k_rs_marks, gn, dim3(FT), 0, s, dev_frames, n, dev_n, a, b, st);
+    if ((rc = hip_err(hipGetLastError()))) return rc;
+  }
+  if ((rc = scan<op_max, false, false>(a, n, part, tot + 2, s))) return rc;
+  if ((rc = scan<op_min, true, false>(b, n, part, tot + 3, s))) return rc;
+  if (n) {
+    hipLaunchKernelGGL(k_rs_sizes, gn, dim3(FT), 0, s, dev_frames, n, dev_n, (const uint64_t*)a,
+                       (const uint64_t*)b, off, cnt, orph);
+    if ((rc = hip_err(hipGetLastError()))) return rc;
+  }
+  if ((rc = scan<op_sum, false, true>(off, n, part, tot + 0, s))) return rc;
+  if ((rc = scan<op_sum, false, true>(cnt, n, part, tot + 2, s))) return rc;
+  if ((rc = scan<op_sum, false, true>(st, n, part, tot + 1, s))) return rc;
+  if ((rc = scan<op_sum, false, true>(orph, n, part, tot + 3, s))) return rc;
+  if (n) {
+    hipLaunchKernelGGL(k_rs_first, gn, dim3(FT), 0, s, dev_frames, n, dev_n, (const uint64_t*)st, dev_msgs,
+                       msg_cap);
+    if ((rc = hip_err(hipGetLastError()))) return rc;
+  }
+  hipLaunchKernelGGL(k_rs_msgs, gn, dim3(FT), 0, s, dev_n, n, (const uint64_t*)(tot + 1), (const uint64_t*)off,
+                     (const uint64_t*)cnt, (const uint64_t*)b, (const uint64_t*)orph, (const uint64_t*)orph,
+                     out_cap, dev_msgs, msg_cap, dev_nmsgs);
+  if ((rc = hip_err(hipGetLastError()))) return rc;
+  const uintptr_t oa = reinterpret_cast<uintptr_t>(dev_out);
+  const uintptr_t sa = reinterpret_cast<uintptr_t>(dev_src);
+  gparams G;
+  G.src = reinterpret_cast<const uint8_t*>(sa & ~(uintptr_t)15);
+  G.src_lo = sa & 15;
+  G.src_len = src_len;
+  G.frames = dev_frames;
+  G.off = off;
+  G.n = n;
+  G.dev_n = dev_n;
+  G.mode = G_REASM;
+  G.flags = 0;
+  G.enc_opts = 0;
+  G.keys = nullptr;
+  G.out = reinterpret_cast<uint8_t*>(oa & ~(uintptr_t)15);
+  G.out_lo = oa & 15;
+  G.out_cap = out_cap;
+  G.err = ctx->err;
+  if (n && out_cap) {
+    const uint64_t tiles = (G.out_lo + out_cap + GTILE - 1) / GTILE;
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(tiles, 1, 8192)), dim3(FT), 0, s, G);
+    if ((rc = hip_err(hipGetLastError()))) return rc;
+  }
+  if ((opts & XYWS_REASM_UTF8) && out_cap && msg_cap) {
+    const uint64_t chunks = (out_cap + 15) / 16;
+    hipLaunchKernelGGL(k_utf8, dim3(grid_for(chunks, FT, 4096)), dim3(FT), 0, s, (const uint8_t*)G.out, G.out_lo,
+                       out_cap, (const uint64_t*)(tot + 1), dev_msgs, msg_cap);
+    if ((rc = hip_err(hipGetLastError()))) return rc;
+  }
+  return XYWS_OK;
+}
+
+}  // extern "C"

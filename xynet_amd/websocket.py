@@ -5,12 +5,17 @@ Names, argument meaning and error behaviour follow the reference headers
 
   websocket_flags                  include/xynet/http/websocket_frame_header.h:42-106
   calc_frame_header_size / _size   :111-131, WS_MAX_FRAME_HEADER_SIZE :134
-  websocket_frame_header           :179-224  (encode side; built on the host, as the
-                                              reference builds reply headers)
-  websocket_frame_header_parser    :226-303  (parse/result/reset/npos over device bytes)
+  websocket_frame_header           :179-224  (xyws_header_build, the reference builder's
+                                              bytes; one header, no device work)
+  websocket_frame_header_parser    :226-385  (xyws_parser_*: parsed on the device)
   websocket_mask                   include/xynet/http/websocket_frame_mask.h:6-25
   frame_decoder.decode             the batched websocket_recv_data
                                    (example/include/common/websocket.h:110-134)
+  encode_frames                    echo_once's replies, batched on the device
+                                   (example/websocket/websocket_echo.cpp:18-27)
+  classify_frames                  websocket_check_parser_result's policy
+                                   (example/include/common/websocket.h:81-108)
+  reassemble                       FIN=0 chains -> messages (+ UTF-8 check)
 
 Device buffers are torch uint8 tensors on a ROCm device (PyTorch is used only
 for device memory and streams). Every computing call runs HIP kernels from
@@ -65,20 +70,13 @@ WS_MAX_FRAME_HEADER_SIZE = calc_frame_header_size(websocket_flags.WS_HAS_MASK, 0
 
 
 def _builder(flags, mask, data_len):
-    """detail::websocket_frame_header_builder (:136-175): returns the header bytes;
-    key bytes are written only when `mask` is given (:168-171)."""
-    flags = int(flags)
-    b0 = (0x80 if flags & websocket_flags.WS_FIN else 0) | (flags & 0x0F)
-    b1 = 0x80 if flags & websocket_flags.WS_HAS_MASK else 0
-    if data_len < 126:
-        out = bytearray([b0, b1 | data_len])
-    elif data_len <= 0xFFFF:
-        out = bytearray([b0, b1 | 126]) + data_len.to_bytes(2, "big")
-    else:
-        out = bytearray([b0, b1 | 127]) + (data_len & ((1 << 64) - 1)).to_bytes(8, "big")
-    if flags & websocket_flags.WS_HAS_MASK:
-        out += bytes(mask) if mask is not None else b"\0\0\0\0"
-    return bytes(out)
+    """detail::websocket_frame_header_builder (:136-175) through xyws_header_build:
+    the header bytes; key bytes are written only when `mask` is given (:168-171)."""
+    L = _lib.load()
+    out = (C.c_uint8 * 16)()
+    key = None if mask is None else (C.c_uint8 * 4)(*bytes(mask))
+    n = L.xyws_header_build(int(flags) & 0xFF, key, int(data_len) & ((1 << 64) - 1), out)
+    return bytes(out[:n])
 
 
 class websocket_frame_header:
@@ -276,53 +274,126 @@ def decode_indexed(buf, starts, frames=True, parse_only=False):
 
 
 class websocket_frame_header_parser:
-    """websocket_frame_header_parser (:226-303) over device-resident bytes.
+    """websocket_frame_header_parser (:226-385) through xyws_parser_* (C-ABI).
 
-    parse(bytes) returns the number of bytes consumed in THIS call up to the
-    end of the header, or ``npos`` while the header is incomplete; once a header
-    completed, further input returns npos until reset() (:305-385). result()
-    returns (flags, mask_uint32_t, length) after a completed header (the
-    reference's usage, websocket.h:121-128). Each call runs the device decoder
-    in parse-only mode; state lives in a device-side xyws_carry.
+    parse(data) takes bytes (host) or a device uint8 tensor and returns the
+    number of bytes consumed in THIS call up to the end of the header, or
+    ``npos`` while the header is incomplete; once a header completed, further
+    input returns npos until reset() (:378-384). result() returns (flags,
+    mask_uint32_t, length) (websocket.h:121-128). The bytes are parsed on the
+    device (stream decoder, parse-only, device-resident carry).
     """
     npos = npos
 
     def __init__(self, device=None):
-        self._dec = frame_decoder(device, parse_only=True)
-        self._finished = False
-        self._res = (websocket_flags.WS_NONE, 0, 0)
+        import torch
+        self.ctx = context(device)
+        self.L = self.ctx.L
+        h = C.c_void_p()
+        check(self.L.xyws_parser_create(self.ctx.h, C.byref(h)), "xyws_parser_create")
+        self.h = h
+        self._stream = C.c_void_p(torch.cuda.current_stream(self.ctx.device).cuda_stream)
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.L.xyws_parser_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
 
     def reset(self):
-        self._dec.reset()
-        self._finished = False
-        self._res = (websocket_flags.WS_NONE, 0, 0)
+        check(self.L.xyws_parser_reset(self.h), "xyws_parser_reset")
 
     def parse(self, data):
-        if self._finished:
-            return npos
-        t = _dev_u8(data)
-        if t.numel() == 0:
-            return npos
-        before = self._dec.carry().hdr_len
-        r = self._dec.decode(t, cap=1)
-        if r.nframes == 0:
-            return npos
-        f = r.frames()[0]
-        self._finished = True
-        self._res = (websocket_flags(f.flags), int.from_bytes(bytes(f.key), "little"), f.payload_len)
-        return f.hdr_len - before
+        import torch
+        consumed = C.c_uint64()
+        if isinstance(data, torch.Tensor):
+            t = _dev_u8(data)
+            ptr, n = C.c_void_p(t.data_ptr()), t.numel()
+            check(self.L.xyws_parser_parse(self.h, ptr, n, C.byref(consumed), _stream(t)), "xyws_parser_parse")
+        else:
+            b = bytes(data)
+            buf = C.create_string_buffer(b, max(len(b), 1))
+            check(self.L.xyws_parser_parse(self.h, buf, len(b), C.byref(consumed), self._stream),
+                  "xyws_parser_parse")
+        return consumed.value
+
+    def _res(self):
+        f, ln = C.c_uint8(), C.c_uint64()
+        key = (C.c_uint8 * 4)()
+        check(self.L.xyws_parser_result(self.h, C.byref(f), key, C.byref(ln)), "xyws_parser_result")
+        return websocket_flags(f.value), int.from_bytes(bytes(key), "little"), ln.value
 
     def flags(self):
-        return self._res[0]
+        return self._res()[0]
 
     def length(self):
-        return self._res[2]
+        return self._res()[2]
 
     def mask_uint32_t(self):
-        return self._res[1]
+        return self._res()[1]
 
     def mask(self):
-        return self._res[1].to_bytes(4, "little")
+        return self._res()[1].to_bytes(4, "little")
 
     def result(self):
-        return self._res
+        return self._res()
+
+
+# ---------------------------------------------------------------------------
+# the callers either side of the decode path (xyws_frames.hip)
+
+def _opt_ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def encode_frames(src, frames_t, n, flags, dev_n=None, enc_opts=0, keys=None, verdicts=None,
+                  action_mask=0, out=None, offsets=None):
+    """echo_once's replies for a decoded frame table, on the device
+    (xyws_encode_frames). src: the decoded batch (device uint8); frames_t:
+    n xyws_frame records (device uint8, n*32 bytes); keys: device uint8 (4 per
+    frame) for client-role masking. Returns (out, out_len tensor)."""
+    import torch
+    t = _dev_u8(src)
+    ctx = context(t.device.index)
+    olen = torch.zeros(1, dtype=torch.int64, device=t.device)
+    if out is None:
+        raise XywsError(-1, "encode_frames needs an output tensor (size it with encode_size)")
+    check(ctx.L.xyws_encode_frames(ctx.h, C.c_void_p(t.data_ptr()), t.numel(), _opt_ptr(frames_t), n,
+                                   _opt_ptr(dev_n), int(flags) & 0xFF, enc_opts, _opt_ptr(keys),
+                                   _opt_ptr(verdicts), action_mask, C.c_void_p(out.data_ptr()), out.numel(),
+                                   _opt_ptr(offsets), C.c_void_p(olen.data_ptr()), _stream(t)),
+          "xyws_encode_frames")
+    return out, olen
+
+
+def classify_frames(src, frames_t, n, max_payload, policy=0, dev_n=None):
+    """websocket_check_parser_result per frame (xyws_classify_frames): returns
+    (verdicts tensor (n*8 bytes), first-close tensor)."""
+    import torch
+    t = _dev_u8(src)
+    ctx = context(t.device.index)
+    verd = torch.zeros(max(n, 1) * 8, dtype=torch.uint8, device=t.device)
+    first = torch.zeros(1, dtype=torch.int64, device=t.device)
+    check(ctx.L.xyws_classify_frames(ctx.h, C.c_void_p(t.data_ptr()), t.numel(), _opt_ptr(frames_t), n,
+                                     _opt_ptr(dev_n), max_payload, policy, C.c_void_p(verd.data_ptr()),
+                                     C.c_void_p(first.data_ptr()), _stream(t)), "xyws_classify_frames")
+    return verd, first
+
+
+def reassemble(src, frames_t, n, opts=0, out_cap=None, msg_cap=None, dev_n=None):
+    """FIN=0 chains gathered into messages (xyws_reassemble): returns (out,
+    messages tensor (msg_cap*40 bytes), count tensor)."""
+    import torch
+    t = _dev_u8(src)
+    ctx = context(t.device.index)
+    cap = t.numel() if out_cap is None else out_cap
+    mcap = max(n, 1) if msg_cap is None else msg_cap
+    out = torch.zeros(max(cap, 1), dtype=torch.uint8, device=t.device)
+    msgs = torch.zeros(max(mcap, 1) * 40, dtype=torch.uint8, device=t.device)
+    cnt = torch.zeros(1, dtype=torch.int64, device=t.device)
+    check(ctx.L.xyws_reassemble(ctx.h, C.c_void_p(t.data_ptr()), t.numel(), _opt_ptr(frames_t), n, _opt_ptr(dev_n),
+                                opts, C.c_void_p(out.data_ptr()), cap, C.c_void_p(msgs.data_ptr()), mcap,
+                                C.c_void_p(cnt.data_ptr()), _stream(t)), "xyws_reassemble")
+    return out, msgs, cnt
