@@ -241,6 +241,62 @@ def host_path_rate(torch, ws, T, info, buf, golden, chunk=256 << 20, reps=3, nst
             "chunk_bytes": per, "passes": reps, "parity": dig == want and err == 0, "device_error": err}
 
 
+def arena_path_rate(torch, ws, T, info, buf, golden, conns=4, recv=16 << 20):
+    """PCIe-inclusive rate through the io_uring-facing API (xyws_arena_*, never
+    the bench value): the batch split at frame boundaries over `conns`
+    connections, each one's bytes in its own pinned arena, submitted in
+    `recv`-byte pieces cut anywhere (the carry chains across them on the
+    device), completions taken from one eventfd with poll() as an io_uring loop
+    would. One pass: the arenas then hold the decoded batch (digest checked)."""
+    import ctypes as C
+    import select
+    size = buf.numel()
+    fb = size // info["nframes"]
+    per = -(-info["nframes"] // conns) * fb
+    fd = os.eventfd(0, os.EFD_NONBLOCK)
+    arenas, plan = [], []
+    for k, off in enumerate(range(0, size, per)):
+        n = min(per, size - off)
+        a = ws.RecvArena(n, max(1, n // fb + 2), eventfd=fd)
+        view = torch.frombuffer((C.c_uint8 * n).from_address(a.host_ptr), dtype=torch.uint8)
+        view.copy_(buf[off:off + n])  # (the masked input, D2H into the pinned arena)
+        arenas.append((a, off, n, view))
+        plan.append([(o, min(recv, n - o)) for o in range(0, n, recv)])
+    torch.cuda.synchronize()
+    poller = select.poll()
+    poller.register(fd, select.POLLIN)
+    pending = [[] for _ in arenas]
+    nxt = [0] * len(arenas)
+    t0 = time.perf_counter()
+    while any(nxt[k] < len(plan[k]) or pending[k] for k in range(len(arenas))):
+        progressed = False
+        for k, (a, _, _, _) in enumerate(arenas):
+            while nxt[k] < len(plan[k]):
+                s = a.submit(*plan[k][nxt[k]])
+                if s is None:
+                    break
+                pending[k].append(s)
+                nxt[k] += 1
+                progressed = True
+            while pending[k] and a.poll(pending[k][0]) is not None:
+                pending[k].pop(0)
+                progressed = True
+        if not progressed and poller.poll(1000):
+            os.eventfd_read(fd)
+    dt = time.perf_counter() - t0
+    chk = torch.empty(size, dtype=torch.uint8, device="cuda")
+    for a, off, n, view in arenas:
+        chk[off:off + n].copy_(view)
+    dig = device_digest(torch, T, chk)
+    err = ws.context().last_device_error()
+    for a, _, _, _ in arenas:
+        a.close()
+    os.close(fd)
+    return {"gibs": round(info["payload_bytes"] / dt / GIB, 3), "connections": len(arenas), "recv_bytes": recv,
+            "api": "xyws_arena_submit / eventfd", "parity": dig == golden["out_digest"] and err == 0,
+            "device_error": err}
+
+
 def source_hash():
     """Hash of the decoder sources, stamped on PMC records (profiles/pmc_traffic.json)
     so that a traffic figure is only reported for the kernel it was measured on."""
@@ -427,6 +483,7 @@ def main():
             cpu = cpu_baseline(torch, bufs[0], info, args.cpu_budget)
         if args.host_path and info["nframes"] and args.config != "c4" and golden is not None:
             host_rate = host_path_rate(torch, ws, T, info, bufs[0], golden)
+            host_rate["arena"] = arena_path_rate(torch, ws, T, info, bufs[0], golden)
 
     traffic, traffic_src = pmc_traffic(args.config, args.mode)
 

@@ -70,6 +70,7 @@ extern "C" {
 #define XYWS_ERR_NOMEM      -3  /* device scratch allocation failed */
 #define XYWS_ERR_CAPACITY   -4  /* batch larger than xyws_ctx_reserve() allowed while capturing */
 #define XYWS_ERR_DEVICE     -5  /* a device-side bound tripped (see xyws_ctx_last_device_error) */
+#define XYWS_ERR_AGAIN      -6  /* not complete yet (xyws_arena_poll) / no free slot (xyws_arena_submit) */
 
 /* ---- websocket_flags encoding (websocket_frame_header.h:42-58) ----------- */
 #define XYWS_FLAG_OP_CONTINUE 0x00
@@ -292,6 +293,51 @@ int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len,
                     const xyws_frame* dev_frames, uint64_t n, const uint64_t* dev_n, uint32_t opts,
                     void* dev_out, uint64_t out_cap, xyws_message* dev_msgs, uint64_t msg_cap,
                     uint64_t* dev_nmsgs, void* stream);
+
+/* ---- recv arenas: the io_uring side (recv_all.h:86-121, io_service.h:362-381)
+ * One arena per connection: a receive area in pinned host memory (allocated
+ * here, or the caller's buffer registered with hipHostRegister, e.g. the
+ * memory an io_uring registered-buffer ring hands to recv), a device mirror,
+ * a device-resident carry and up to XYWS_ARENA_SLOTS submissions in flight on
+ * the arena's own HIP stream. xyws_arena_submit(offset, len) enqueues
+ * H2D -> xyws_decode_stream (carry chained across submissions, so a frame cut
+ * by a recv boundary decodes as if unsplit) -> D2H of the unmasked bytes back
+ * into the same host range (in place, like websocket_mask) and of the frame
+ * table and count, then a host callback that marks the submission complete
+ * and writes 1 to the arena's eventfd (when one is given): the ring keeps a
+ * poll_add on that fd exactly as io_service does for its remote-queue eventfd
+ * and never blocks on the GPU. xyws_arena_poll() returns XYWS_ERR_AGAIN until
+ * the submission completed. Submissions complete in order. A submission's
+ * results stay valid until its slot is reused, which happens only after
+ * poll() or wait() returned them: submit() returns XYWS_ERR_AGAIN while
+ * XYWS_ARENA_SLOTS submissions are in flight or unclaimed. */
+#define XYWS_ARENA_SLOTS 8
+typedef struct xyws_arena xyws_arena;
+typedef struct xyws_arena_result {
+  uint64_t seq;              /* the submission */
+  uint64_t offset, len;      /* its host range (now unmasked in place) */
+  uint64_t nframes;          /* frames whose header completed in it */
+  const xyws_frame* frames;  /* min(nframes, max_frames) descriptors, pinned host memory, offsets
+                                relative to `offset`; valid until the slot is reused */
+  xyws_carry carry;          /* the connection's carry after it */
+} xyws_arena_result;
+/* host == NULL: allocate `bytes` of pinned memory; else register the caller's
+ * host range (unregistered at destroy). eventfd < 0: no notification. */
+int xyws_arena_create(xyws_ctx* ctx, void* host, uint64_t bytes, uint64_t max_frames, int eventfd,
+                      xyws_arena** out);
+int xyws_arena_destroy(xyws_arena* a);
+void* xyws_arena_host(xyws_arena* a);
+int xyws_arena_submit(xyws_arena* a, uint64_t offset, uint64_t len, uint32_t opts, uint64_t* seq);
+int xyws_arena_poll(xyws_arena* a, uint64_t seq, xyws_arena_result* out);
+int xyws_arena_wait(xyws_arena* a, uint64_t seq, xyws_arena_result* out);
+/* The completion notifier on its own (no device): what the arena's host
+ * callback runs. Exposed so the eventfd handshake can be exercised on a host
+ * without a GPU. */
+typedef struct xyws_notifier xyws_notifier;
+int xyws_notifier_create(int eventfd, xyws_notifier** out);
+int xyws_notifier_destroy(xyws_notifier* n);
+int xyws_notifier_signal(xyws_notifier* n, uint64_t seq); /* marks seq complete, writes the fd */
+uint64_t xyws_notifier_completed(const xyws_notifier* n); /* highest completed seq + 1 */
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -26,7 +26,7 @@ OPT_TEST_STEAL = 0x800000
 # debug stats indices (xyws_stream.hip)
 ST_GIVEUP, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS = 32, 33, 34, 35, 36
 ERRORS = {-1: "invalid argument", -2: "HIP runtime error", -3: "device allocation failed",
-          -4: "scratch capacity exceeded", -5: "device-side error"}
+          -4: "scratch capacity exceeded", -5: "device-side error", -6: "not complete yet"}
 
 
 class XywsError(RuntimeError):
@@ -64,7 +64,16 @@ class Message(C.Structure):
                 ("reserved", C.c_uint8 * 3)]
 
 
+class ArenaResult(C.Structure):
+    """xyws_arena_result (include/xyws.h)."""
+    _fields_ = [("seq", C.c_uint64), ("offset", C.c_uint64), ("len", C.c_uint64), ("nframes", C.c_uint64),
+                ("frames", C.POINTER(Frame)), ("carry", Carry)]
+
+
 assert C.sizeof(Frame) == 32 and C.sizeof(Carry) == 64
+assert C.sizeof(ArenaResult) == 104
+XYWS_ERR_AGAIN = -6
+ARENA_SLOTS = 8
 assert C.sizeof(Verdict) == 8 and C.sizeof(Message) == 40
 NPOS = (1 << 64) - 1
 ENC_FRAME_OPCODE = 0x1
@@ -80,7 +89,7 @@ _tools = None
 def declared_symbols(header=HEADER):
     """Function names declared in include/xyws.h."""
     src = open(header).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*|uint64_t|void)\s+(xyws_\w+)\s*\(",
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*|uint64_t|void\s*\*|void)\s*(xyws_\w+)\s*\(",
                                  src, re.M)))
 
 
@@ -140,6 +149,26 @@ def load():
     L.xyws_classify_frames.argtypes = [vp, vp, u64, vp, u64, vp, u64, u32, vp, vp, vp]
     L.xyws_reassemble.restype = i32
     L.xyws_reassemble.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp, u64, vp, u64, vp, vp]
+    L.xyws_arena_create.restype = i32
+    L.xyws_arena_create.argtypes = [vp, vp, u64, u64, i32, C.POINTER(vp)]
+    L.xyws_arena_destroy.restype = i32
+    L.xyws_arena_destroy.argtypes = [vp]
+    L.xyws_arena_host.restype = vp
+    L.xyws_arena_host.argtypes = [vp]
+    L.xyws_arena_submit.restype = i32
+    L.xyws_arena_submit.argtypes = [vp, u64, u64, u32, C.POINTER(u64)]
+    L.xyws_arena_poll.restype = i32
+    L.xyws_arena_poll.argtypes = [vp, u64, vp]
+    L.xyws_arena_wait.restype = i32
+    L.xyws_arena_wait.argtypes = [vp, u64, vp]
+    L.xyws_notifier_create.restype = i32
+    L.xyws_notifier_create.argtypes = [i32, C.POINTER(vp)]
+    L.xyws_notifier_destroy.restype = i32
+    L.xyws_notifier_destroy.argtypes = [vp]
+    L.xyws_notifier_signal.restype = i32
+    L.xyws_notifier_signal.argtypes = [vp, u64]
+    L.xyws_notifier_completed.restype = u64
+    L.xyws_notifier_completed.argtypes = [vp]
     _lib = L
     return L
 

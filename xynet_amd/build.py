@@ -19,7 +19,7 @@ COMMON = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-W
           "-Wno-unused-function", "-I" + INC, "-I" + CSRC]
 
 TARGETS = {
-    "libxyws.so": ["xyws.hip", "xyws_stream.hip", "xyws_frames.hip"],
+    "libxyws.so": ["xyws.hip", "xyws_stream.hip", "xyws_frames.hip", "xyws_arena.hip"],
     "libxyws_tools.so": ["xyws_tools.hip"],
 }
 DEPS = ["xyws_device.h", "xyws_stream.h", "xyws_ctx.h"]

@@ -277,6 +277,7 @@ const char* xyws_strerror(int code) {
     case XYWS_ERR_NOMEM: return "device allocation failed";
     case XYWS_ERR_CAPACITY: return "scratch capacity exceeded";
     case XYWS_ERR_DEVICE: return "device-side error";
+    case XYWS_ERR_AGAIN: return "not complete yet";
     default: return "unknown error";
   }
 }

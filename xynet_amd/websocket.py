@@ -397,3 +397,61 @@ def reassemble(src, frames_t, n, opts=0, out_cap=None, msg_cap=None, dev_n=None)
                                 opts, C.c_void_p(out.data_ptr()), cap, C.c_void_p(msgs.data_ptr()), mcap,
                                 C.c_void_p(cnt.data_ptr()), _stream(t)), "xyws_reassemble")
     return out, msgs, cnt
+
+
+class RecvArena:
+    """A connection's receive arena (xyws_arena_*): recv into pinned host
+    memory, decode on the device with the connection's carry, results and the
+    unmasked bytes back in place; each completion writes 1 to `eventfd` (the
+    fd an io_uring loop keeps a poll_add on, io_service.h:362-381)."""
+
+    def __init__(self, nbytes, max_frames, eventfd=-1, device=None, host=None):
+        self.ctx = context(device)
+        self.L = self.ctx.L
+        h = C.c_void_p()
+        check(self.L.xyws_arena_create(self.ctx.h, host, nbytes, max_frames, eventfd, C.byref(h)),
+              "xyws_arena_create")
+        self.h = h
+        self.nbytes = nbytes
+        self.max_frames = max_frames
+        self.host_ptr = self.L.xyws_arena_host(h)
+
+    def view(self):
+        """The receive area as a writable memoryview (pinned host memory)."""
+        return (C.c_uint8 * self.nbytes).from_address(self.host_ptr)
+
+    def submit(self, offset, length, opts=0):
+        seq = C.c_uint64()
+        rc = self.L.xyws_arena_submit(self.h, offset, length, opts, C.byref(seq))
+        if rc == _lib.XYWS_ERR_AGAIN:
+            return None
+        check(rc, "xyws_arena_submit")
+        return seq.value
+
+    def poll(self, seq):
+        res = _lib.ArenaResult()
+        rc = self.L.xyws_arena_poll(self.h, seq, C.byref(res))
+        if rc == _lib.XYWS_ERR_AGAIN:
+            return None
+        check(rc, "xyws_arena_poll")
+        return res
+
+    def wait(self, seq):
+        res = _lib.ArenaResult()
+        check(self.L.xyws_arena_wait(self.h, seq, C.byref(res)), "xyws_arena_wait")
+        return res
+
+    @staticmethod
+    def frames_of(res, max_frames):
+        return [res.frames[i] for i in range(min(res.nframes, max_frames))]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.xyws_arena_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
