@@ -4,7 +4,9 @@
 HBM traffic per k_stream_runs launch (the dominant kernel of xyws_decode_stream), per MI355X_MICROARCH.md §HBM: gfx950's
 FETCH_SIZE reports half the bytes of wide coalesced streaming reads (doubled
 here); WRITE_SIZE reads the bytes exactly for 16-B-per-lane stores. Both
-counters are in KiB. Usage: pmc_summary.py FETCH_DIR WRITE_DIR KEY [OUT]
+counters are in KiB. Usage: pmc_summary.py FETCH_DIR WRITE_DIR KEY PROFILE [OUT]
+KEY is "<config>:<mode>"; the record is stamped with the decoder sources' hash
+(bench.source_hash) so bench.py only reports traffic measured on this kernel.
 """
 import csv
 import glob
@@ -24,9 +26,19 @@ def per_launch(d, counter, kernel="k_stream_runs"):
     return sum(vals) / len(vals), len(vals)
 
 
+def source_hash():
+    import hashlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    h = hashlib.sha256()
+    for f in ("xyws_stream.hip", "xyws_device.h", "xyws_stream.h", "xyws.hip"):
+        with open(os.path.join(root, "xynet_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def main():
-    fdir, wdir, key = sys.argv[1:4]
-    out = sys.argv[4] if len(sys.argv) > 4 else os.path.join(
+    fdir, wdir, key, profile = sys.argv[1:5]
+    out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
     fk, nf = per_launch(fdir, "FETCH_SIZE")
     wk, nw = per_launch(wdir, "WRITE_SIZE")
@@ -36,6 +48,8 @@ def main():
         "hbm_write_bytes_per_launch": int(wk * 1024),
         "hbm_bytes_per_launch": int(fk * 2 * 1024 + wk * 1024),
         "correction": "FETCH_SIZE x2 (gfx950 streaming-read undercount), KiB -> bytes",
+        "src_sha": source_hash(),
+        "profile": profile,
     }
     data = json.load(open(out)) if os.path.exists(out) else {}
     data[key] = rec

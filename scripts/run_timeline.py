@@ -40,7 +40,8 @@ def main():
     for i, r in enumerate(recs):
         if not r[25]:
             continue
-        rows.append(dict(run=i // 2, piece=i & 1, start=(r[25] - base) / 100.0, prologue=(r[26] - r[25]) / 100.0 if r[26] else None,
+        rows.append(dict(run=i // 2, piece=i & 1, xcc=r[29], start=(r[25] - base) / 100.0,
+                         prologue=(r[26] - r[25]) / 100.0 if r[26] else None,
                          end=(r[27] - base) / 100.0 if r[27] else None))
     ends = [x["end"] for x in rows if x["end"] is not None]
     pros = [x["prologue"] for x in rows if x["prologue"] is not None]
@@ -51,6 +52,18 @@ def main():
            "end_us": [round(min(ends), 2), round(statistics.mean(ends), 2), round(statistics.median(ends), 2),
                       round(max(ends), 2)],
            "latest_runs": sorted(rows, key=lambda x: -(x["end"] or 0))[:8]}
+    by_xcc = {}
+    for x in rows:
+        if x["end"] is not None and not x["piece"]:
+            by_xcc.setdefault(x["xcc"], []).append(x["end"])
+    out["end_us_by_xcc"] = {k: [len(v), round(min(v), 1), round(statistics.mean(v), 1), round(max(v), 1)]
+                            for k, v in sorted(by_xcc.items())}
+    # which part of a run's range: the end time against the run index mod 8 / 32
+    by_mod = {}
+    for x in rows:
+        if x["end"] is not None and not x["piece"]:
+            by_mod.setdefault(x["run"] % 8, []).append(x["end"])
+    out["end_us_by_run_mod8"] = {k: round(statistics.mean(v), 1) for k, v in sorted(by_mod.items())}
     print(json.dumps(out))
 
 

@@ -147,6 +147,7 @@ enum {
   R_EP = 24,                                        // epoch of the call that wrote the results
   R_T0, R_T1, R_T2,                                 // stats mode: s_memrealtime at start, after the prologue, at the end
   R_SPLIT,                                          // own runs: the split segment a thief took the rest from (NONE: none)
+  R_XCC,                                            // stats mode: the XCD (XCC_ID) the run's workgroup ran on
   R_WORDS = 32
 };
 // R_OK bits
@@ -1683,6 +1684,7 @@ XYWS_DEV void finish_fast(const run_params& P, lds_t<G>& L, uint32_t tid) {
   __syncthreads();
   const uint64_t E = L.E;
   const uint32_t lane = tid & 63u, wave = tid >> 6;
+  const bool plan = P.frames && P.cap;  // (the descriptor plan is read by k_stream_emit only)
   uint64_t carry = 0;
   uint32_t bad = 0, stale = 0, last = 0;
   bool has = false;
@@ -1727,7 +1729,7 @@ XYWS_DEV void finish_fast(const run_params& P, lds_t<G>& L, uint32_t tid) {
       if (w < wave) wb += v;
       tot += v;
     }
-    if (vis && XYWS_EXP_FINISH != 3) {
+    if (vis && plan && XYWS_EXP_FINISH != 3) {
       uint64_t* rw = P.rec + (uint64_t)r * R_WORDS;
       st_store(rw + R_EFROM, h);
       st_store(rw + R_ECNT, cnt);
@@ -1881,7 +1883,11 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
       L.split_e = NONE;
       L.self = 2 * (uint64_t)run;
       L.rs = rs;
-      if (stats_on(P)) st_store(rec + R_T0, __builtin_amdgcn_s_memrealtime());
+      if (stats_on(P)) {
+        st_store(rec + R_T0, __builtin_amdgcn_s_memrealtime());
+        // HW_REG_XCC_ID (hwreg 20), bits [3:0]
+        st_store(rec + R_XCC, (uint64_t)(__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xFu));
+      }
       if (run == 0) {
         // snapshot of the incoming carry for k_stream_finish / k_stream_emit
         // (the caller's carry may alias the carry out, which finish writes)
@@ -1897,7 +1903,13 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
         uint64_t c0;
         L.S = initial_state(P, &cz, c0);
         L.cnt = c0;
-        L.dense = 0;
+        // dense-pass hint for the first segment, as a prologue sets it: the
+        // frame at the first boundary is small (run 0 chased its first
+        // segment serially before: the slowest run of a small-frame batch)
+        {
+          const hdr_info h0 = (L.S.st & S_PARTIAL) ? hdr_info{} : hdr_global(P, L.S.X, NONE);
+          L.dense = (h0.hlen && h0.plen + h0.hlen < 1024) ? G::FCAP : 0;
+        }
         st_store(rec + R_H, P.lo);
         st_store(rec + R_W, P.lo);
         put_state(rec + R_S0, L.S);
