@@ -277,7 +277,7 @@ enum { ST_RUNS = 0, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRA
        ST_P_WIN, ST_P_CAND, ST_P_UND, ST_P_TCOMP, ST_P_TCHECK, ST_P_TRES, ST_D_TENT, ST_D_TCHASE,
        ST_T_PRO = 16, ST_T_MAIN, ST_T_WAIT, ST_T_FILL, ST_T_CHASE, ST_T_XOR, ST_T_TAIL, ST_T_PF, ST_T_CP,
        ST_P_FILL, ST_P_SCAN, ST_P_PUB, ST_D_NOENT, ST_D_CHASE, ST_D_MISMATCH, ST_D_OVF,
-       ST_GIVEUP = 32, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS };
+       ST_GIVEUP = 32, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS, ST_D_TVAL, ST_T_ROWS, ST_T_SER };
 XYWS_DEV void stat_add(const run_params& P, uint32_t i, uint64_t v) {
   if (stats_on(P)) atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + i, (unsigned long long)v);
 }
@@ -831,6 +831,11 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
     }
   }
   __syncthreads();
+  if (st_on) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    stat_add(P, ST_D_TVAL, t - tq);
+    tq = t;
+  }
   const uint32_t total = L.ccnt;
   if (total == NONE32) return false;
   // 4. compaction (each thread moves at most one entry) and the chain state
@@ -1127,11 +1132,17 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
         // lane 0 chases; then wave 0 classifies the rows (the other waves wait
         // at the barrier with their prefetch in flight: work here is hidden,
         // work in the store loop below is not)
+        const uint64_t t_r0 = st_on ? __builtin_amdgcn_s_memtime() : 0;
         if (tid == 0 && !dense) chase_pass(P, L, ss, lo_c, keep);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint64_t t_r1 = st_on ? __builtin_amdgcn_s_memtime() : 0;
         build_rows<G>(L, L.nfl, lo_c, L.pass_hi, wl_r, wh_r, any, tid);
+        if (st_on && tid == 0) {
+          stat_add(P, ST_T_SER, t_r1 - t_r0);
+          stat_add(P, ST_T_ROWS, __builtin_amdgcn_s_memtime() - t_r1);
+        }
       }
       XYWS_STAMP(acc_cp);
       __syncthreads();
