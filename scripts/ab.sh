@@ -8,7 +8,8 @@ if [ "$mode" = variant ]; then  # scripts/ab.sh variant NAME "-DFLAG=..." : the 
   name=$1; shift
   mkdir -p exp
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-function \
-    -Iinclude -Ixynet_amd/csrc $@ xynet_amd/csrc/xyws.hip xynet_amd/csrc/xyws_stream.hip -o "exp/libxyws_$name.so" || exit 1
+    -Iinclude -Ixynet_amd/csrc $@ xynet_amd/csrc/xyws.hip xynet_amd/csrc/xyws_stream.hip xynet_amd/csrc/xyws_frames.hip \
+    xynet_amd/csrc/xyws_arena.hip -o "exp/libxyws_$name.so" || exit 1
   echo "built exp/libxyws_$name.so"; exit 0
 fi
 if [ "$mode" = build ]; then
@@ -16,11 +17,14 @@ if [ "$mode" = build ]; then
   for rev in "$@"; do
     d=exp/src_$rev; rm -rf "$d"; mkdir -p "$d/include" "$d/csrc"
     git show "$rev:include/xyws.h" > "$d/include/xyws.h" || exit 1
-    for f in xyws.hip xyws_stream.hip xyws_stream.h xyws_device.h; do
-      git show "$rev:xynet_amd/csrc/$f" > "$d/csrc/$f" || exit 1
+    git show "$rev:include/xyws_synth.h" > "$d/include/xyws_synth.h" 2>/dev/null
+    srcs=""
+    for f in $(git ls-tree --name-only "$rev" xynet_amd/csrc/); do
+      f=$(basename "$f"); git show "$rev:xynet_amd/csrc/$f" > "$d/csrc/$f" || exit 1
+      case $f in *.hip) [ "$f" != xyws_tools.hip ] && srcs="$srcs $d/csrc/$f";; esac
     done
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-function \
-      -I"$d/include" -I"$d/csrc" "$d/csrc/xyws.hip" "$d/csrc/xyws_stream.hip" -o "exp/libxyws_$rev.so" || exit 1
+      -I"$d/include" -I"$d/csrc" $srcs -o "exp/libxyws_$rev.so" || exit 1
     echo "built exp/libxyws_$rev.so"
   done
   exit 0

@@ -9,14 +9,15 @@ if [ "$mode" = build ]; then
     name=${v%%:*}; flags=${v#*:}
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-function \
       -Iinclude -Ixynet_amd/csrc $flags xynet_amd/csrc/xyws.hip xynet_amd/csrc/xyws_stream.hip \
-      -o exp/libxyws_$name.so || exit 1
+      xynet_amd/csrc/xyws_frames.hip xynet_amd/csrc/xyws_arena.hip -o exp/libxyws_$name.so || exit 1
   done
   exit 0
 fi
-for rep in 1 2; do
+for rep in $(seq ${REPS:-2}); do
 for name in "$@"; do
   for cfg in ${CFGS:-c3 c1}; do
-    echo "$name $cfg $(XYWS_LIB=$PWD/exp/libxyws_$name.so timeout -k 10 120 python bench.py --config $cfg --steps 20 --warmup 3 --no-cpu 2>/dev/null | grep -o '"ms_per_step": [0-9.]*\|"kernel_ms_avg": [0-9.]*\|"parity": [a-z]*' | tr '\n' ' ')"
+    lib=$PWD/exp/libxyws_$name.so; [ "$name" = cur ] && lib=$PWD/xynet_amd/libxyws.so
+    echo "$name $cfg $(XYWS_LIB=$lib timeout -k 10 120 python bench.py --config $cfg --steps 20 --warmup 3 --no-cpu 2>/dev/null | grep -o '"ms_per_step": [0-9.]*\|"kernel_ms_avg": [0-9.]*\|"parity": [a-z]*' | tr '\n' ' ')"
   done
 done
 done

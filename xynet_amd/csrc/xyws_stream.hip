@@ -31,7 +31,7 @@
 //    exactly on h_r, run r's entry is exact; by induction from run 0 (exact:
 //    batch start and carry) every run is exact when every boundary matches.
 //  * A mismatch (rare: an implausible true header, or a plausible false chain)
-//    is repaired by k_stream_finish: undo the mis-speculated run (replaying its
+//    is repaired by finish_call: undo the mis-speculated run (replaying its
 //    own chain XORs its payloads back; a chain never writes its own headers),
 //    then redo its range from the exact chain, boundary after boundary until the
 //    chains agree again. Speculation decides speed only: any byte stream (RSV
@@ -47,7 +47,7 @@
 // bytes are read only where no other workgroup writes: below the successor's W
 // (a header that would cross it stops the chase, "cut"), or in the run's own
 // range. Flags and the ticket are zeroed when scratch is allocated and reset by
-// k_stream_finish after every call (so a captured graph replays correctly);
+// finish_call after every call (so a captured graph replays correctly);
 // spins are bounded and report through the device error word.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -60,9 +60,9 @@
 namespace {
 
 
-#ifndef XYWS_EXP_FINISH
-#define XYWS_EXP_FINISH 0  // timing experiments (scripts/ab.sh variants): 1 = no repair walk, 2 = no fast path,
-                           // 3 = no descriptor plan stores, 4 = no outputs
+
+#ifndef XYWS_EXP_NODMA
+#define XYWS_EXP_NODMA 0  // timing experiments (scripts/exp_variants.sh): 1 = first segment through registers
 #endif
 
 constexpr uint64_t NONE = ~0ull;
@@ -131,7 +131,7 @@ struct cstate {
   uint32_t pad;
 };
 
-// k_stream_finish's walk: the current chain piece (see the walk below).
+// finish_walk: the current chain piece (see the walk below).
 struct walk_t {
   cstate F;
   uint64_t r, efrom, cnt, tail, first, succ, wlim;
@@ -143,7 +143,7 @@ enum {
   R_H = 0, R_W, R_S0, R_HEAD = R_S0 + 5,            // prologue: entry, write start, state, head frames
   R_OK = 8, R_HN, R_WN, R_CNT, R_TAIL, R_FIRST,     // results (R_OK: ok | tmo << 1 | succ << 32)
   R_F0 = 14,                                        // final state (5 words)
-  R_EFROM = 20, R_ECNT, R_EORD, R_ECARRY,           // emission plan (k_stream_finish)
+  R_EFROM = 20, R_ECNT, R_EORD, R_ECARRY,           // emission plan (finish_call)
   R_EP = 24,                                        // epoch of the call that wrote the results
   R_T0, R_T1, R_T2,                                 // stats mode: s_memrealtime at start, after the prologue, at the end
   R_SPLIT,                                          // own runs: the split segment a thief took the rest from (NONE: none)
@@ -164,7 +164,7 @@ constexpr uint64_t OK_BIT = 1, TMO_BIT = 2;  // chain landed on the successor; s
 //   word 1 (published): h (46 bits, G_NONE = no entry) | (W - h) << 46 (5
 //           bits: W = round16(h + header)) | (E mod 2^13) << 51, the tag a
 //           torn read would fail.
-// The run's record (R_H, R_W, entry state, ...) is for k_stream_finish only,
+// The run's record (R_H, R_W, entry state, ...) is for finish_call only,
 // so the publish needs no wait for the record stores (nor for the prefetch
 // loads in flight).
 XYWS_DEV uint64_t flag_claimed(uint64_t E) { return E << 1; }
@@ -172,6 +172,11 @@ XYWS_DEV uint64_t flag_published(uint64_t E) { return (E << 1) | 1u; }
 constexpr uint64_t G_NONE = (1ull << 46) - 1;
 XYWS_DEV uint64_t granule_tag(uint64_t E) { return (E & 0x1FFFull) << 51; }
 constexpr uint32_t HEAD_EPOCH = 4;   // u32 index of the u64 epoch word in head[]
+// End-of-call words (u64 indices in head[], bytes 512..576), zeroed at
+// allocation and reset by the workgroup that finishes the call: workgroups
+// done, hand-overs that need the repair walk, frames of all items, and the
+// final chain state of the item whose chain reached the batch end.
+constexpr uint32_t HW_DONE = 64, HW_BAD = 65, HW_TOTAL = 66, HW_FINAL = 67;
 
 XYWS_DEV void granule_store(uint64_t* g, uint64_t a, uint64_t b) {
   const u32x4 v = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
@@ -239,10 +244,10 @@ struct __attribute__((aligned(16))) lds_t {
     };
   };
   cstate S;
-  cstate B;  // k_stream_finish: exact state handed to a repaired run
+  cstate B;  // finish_call: exact state handed to a repaired run
   uint64_t hn, Wn, succ, first_after, cnt, tail, aux0, aux1, aux2, bcnt, bfirst;
   uint64_t E;      // this call's epoch
-  xyws_carry cinc; // k_stream_finish: the incoming-carry snapshot
+  xyws_carry cinc; // finish_call: the incoming-carry snapshot
   uint64_t scan_j; // successor lookup: next flat index to examine
   uint64_t ib, ie;     // the item (own run or piece) the workgroup decodes next: its byte range
   uint64_t rng_end;    // end of the current run's range (a run's shrinks when a thief takes its tail)
@@ -251,9 +256,9 @@ struct __attribute__((aligned(16))) lds_t {
   uint64_t split_poll[2] __attribute__((aligned(16)));  // LDS-DMA target: the run's split word
   uint64_t self;       // flat index of the run or piece being decoded
   uint32_t victim;     // 1: the current run answers steal requests (an own run, not yet closed)
-  walk_t wk;       // k_stream_finish: the current chain piece
+  walk_t wk;       // finish_call: the current chain piece
   uint32_t nfl, pass_hi, known, past, ok, done, end, best, ticket, act, repaired, ccnt, ucnt, keepn, ovf;
-  uint32_t tmo;    // successor given up on (write limit = own range end, bridged by k_stream_finish)
+  uint32_t tmo;    // successor given up on (write limit = own range end, bridged by finish_call)
   // per 1 KiB row of the segment (one wave-instruction of chunks), set by
   // wave 0 after each chase pass: ROW_FAST (one key word for the whole row,
   // rk), ROW_SKIP (nothing to store) or the entry to start the walk from
@@ -493,6 +498,40 @@ struct seg_io {
     for (uint32_t k = 0; k < G::CH; k++)
       e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16u, k * G::NT * 16u, AUX_NT);
     pf = ss;
+  }
+  // A run's first segment straight into LDS (LDS-DMA, 16 bytes per lane, the
+  // same chunk layout as fill) and the next segment's loads into the registers
+  // behind it, both in flight at once: the first segment is scanned while the
+  // second one streams in. The DMA loads are invisible to the compiler (asm:
+  // no implicit wait for them before the LDS reads, which would also wait for
+  // the prefetch); the explicit vmcnt(CH) leaves only the prefetch in flight
+  // (vector memory ops complete in issue order). Caller syncs after.
+  XYWS_DEV void fill_dma_and_issue(const run_params& P, lds_t<G>& L, uint64_t ss_in, uint32_t tid) {
+    const uint64_t ss = uniform64(ss_in);
+    // the buffer descriptor of seg_rsrc as four SGPRs (words readfirstlane'd:
+    // the asm operand must be scalar)
+    uint64_t top = (P.hi + 15) & ~15ull;
+    const uint64_t room = top > ss ? top - ss : 0;
+    const uint64_t a = (uint64_t)(uintptr_t)(P.base + ss);
+    u32x4 rs;
+    rs.x = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    rs.y = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xFFFFu);
+    rs.z = __builtin_amdgcn_readfirstlane(room >= G::SEG ? G::SEG : (uint32_t)room);
+    rs.w = 0x00020000u;
+    const uint32_t wave_lds = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)&L.seg[(tid & ~63u) * 16u]);
+#pragma unroll
+    for (uint32_t k = 0; k < G::CH; k++) {
+      asm volatile("s_mov_b32 m0, %1\n\tbuffer_load_dwordx4 %0, %2, %3 offen nt lds"
+                   :: "v"(tid * 16u), "s"(wave_lds + k * G::NT * 16u), "s"(rs), "s"(k * G::NT * 16u)
+                   : "memory", "m0");
+    }
+    const bool more = ss + G::SEG < P.hi;
+    if (more) issue(P, ss + G::SEG, tid);
+    if (more)
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(G::CH) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   // the segment at ss into LDS (caller syncs before and after)
   XYWS_DEV void fill(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid) {
@@ -935,7 +974,7 @@ XYWS_DEV bool wait_published(const run_params& P, uint32_t j, uint64_t E, uint64
 // deadlock), or its bounded wait timed out (reported in the error word). A
 // piece exists only when its run agreed to the split; its thief is running,
 // so it is waited for. Never uses a granule not published in this call. A
-// run given up on is bridged by k_stream_finish.
+// run given up on is bridged by finish_call.
 enum { LK_FOUND = 0, LK_GIVEUP = 1 };
 template <class G>
 XYWS_DEV uint32_t lookup_successor(const run_params& P, lds_t<G>& L, uint64_t& hn, uint64_t& Wn, uint64_t& succ) {
@@ -1066,7 +1105,7 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
       uint64_t hn = NONE, Wn = NONE, succ = P.nflat;
       if (lookup_successor(P, L, hn, Wn, succ) == LK_GIVEUP) {
         // unknown successor: write up to the own range end only and leave
-        // the rest to k_stream_finish (never a stale record)
+        // the rest to finish_call (never a stale record)
         L.hn = NONE; L.Wn = L.rng_end; L.succ = succ; L.known = 1; L.tmo = 1;
       } else {
         L.hn = hn; L.Wn = Wn; L.succ = succ; L.known = 1;
@@ -1499,7 +1538,8 @@ XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32
   uint64_t tp = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
   for (uint64_t ss = rb; ss < re; ss += G::SEG) {
     __syncthreads();
-    io.fill(P, L, ss, tid);
+    if (!XYWS_EXP_NODMA && io.pf == NONE && !(P.opts & XYWS_OPT_DIAG)) io.fill_dma_and_issue(P, L, ss, tid);
+    else io.fill(P, L, ss, tid);
     if (tid == 0) { L.best = 0xFFFFFFFFu; L.aux1 = ss; }
     __syncthreads();
     if (stats_on(P) && tid == 0) {
@@ -1511,7 +1551,7 @@ XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32
     // the entry is in this segment, the scan continues there when it is not
     // (HBM would idle during the scan otherwise; the few header reads from
     // memory below and the publish's vmcnt(0) wait for them)
-    if (ss + G::SEG < P.hi && !(P.opts & XYWS_OPT_DIAG)) io.issue(P, ss + G::SEG, tid);
+    if (ss + G::SEG < P.hi && !(P.opts & XYWS_OPT_DIAG) && io.pf != ss + G::SEG) io.issue(P, ss + G::SEG, tid);
     scan_segment<G>(P, L, ss, tid, unm);
     if (stats_on(P) && tid == 0) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -1631,7 +1671,7 @@ XYWS_DEV void write_outputs(const run_params& P, const xyws_carry* cin, uint64_t
   c[7] = 0;
 }
 
-// k_stream_finish's fast path (whole workgroup; every run has exited). When
+// finish_call's record scan (whole workgroup; every run has exited). When
 // every run with an entry landed exactly on its successor's published entry
 // (the usual case): frame counts, descriptor ordinals and the final state by a
 // block-wide scan over the run records, no serial walk; L.act = 0, L.aux2 =
@@ -1740,7 +1780,7 @@ XYWS_DEV void finish_fast(const run_params& P, lds_t<G>& L, uint32_t tid) {
       if (w < wave) wb += v;
       tot += v;
     }
-    if (vis && plan && XYWS_EXP_FINISH != 3) {
+    if (vis && plan) {
       uint64_t* rw = P.rec + (uint64_t)r * R_WORDS;
       st_store(rw + R_EFROM, h);
       st_store(rw + R_ECNT, cnt);
@@ -1800,6 +1840,12 @@ XYWS_DEV void decode_range(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint
     st_store(rec + R_FIRST, L.first_after);
     put_state(rec + R_F0, L.S);
     st_store(rec + R_EP, L.E);
+    // what the workgroup finishing the call needs when every hand-over is
+    // good: the frame total and the final state (the item without successor)
+    uint64_t* hw = reinterpret_cast<uint64_t*>(P.head);
+    if (!ok) __hip_atomic_fetch_or(hw + HW_BAD, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (L.cnt) __hip_atomic_fetch_add(hw + HW_TOTAL, L.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ok && L.succ >= P.nflat) put_state(hw + HW_FINAL, L.S);
     if (stats_on(P)) st_store(rec + R_T2, __builtin_amdgcn_s_memrealtime());
     if (!ok) stat_add(P, ST_BAD, 1);
     if (L.tmo) stat_add(P, ST_GIVEUP, 1);
@@ -1868,6 +1914,9 @@ XYWS_DEV uint32_t steal_piece(const run_params& P, lds_t<G>& L, uint32_t tid) {
 // pieces of slower runs (steal_piece) until none is worth taking; the run /
 // piece loop keeps one copy of the prologue and of the chain in the kernel.
 template <class G>
+__device__ __attribute__((noinline)) void finish_call(run_params P, lds_t<G>& L, uint32_t tid);
+
+template <class G>
 __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
   lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
@@ -1884,7 +1933,7 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
     const uint64_t rs = (uint64_t)run * P.rbytes;
     uint64_t* rec = P.rec + 2 * (uint64_t)run * R_WORDS;
     if (tid == 0) {
-      // no descriptors unless k_stream_finish plans them (the run and its piece)
+      // no descriptors unless finish_call plans them (the run and its piece)
       st_store(rec + R_ECNT, 0);
       st_store(rec + R_WORDS + R_ECNT, 0);
       st_store(rec + R_SPLIT, NONE);
@@ -1900,7 +1949,7 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
         st_store(rec + R_XCC, (uint64_t)(__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xFu));
       }
       if (run == 0) {
-        // snapshot of the incoming carry for k_stream_finish / k_stream_emit
+        // snapshot of the incoming carry for finish_call / k_stream_emit
         // (the caller's carry may alias the carry out, which finish writes)
         xyws_carry cz;
         if (P.cin_user) {
@@ -1987,6 +2036,15 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
     }
     __syncthreads();
   }
+  // End of the workgroup: its records and end-of-call words have landed (sc1
+  // stores and atomics, vmcnt 0), then one done-count add; the workgroup whose
+  // add comes last finishes the call (no second kernel on the stream).
+  if (tid0 == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    L.act = atomicAdd(P.head + 2 * HW_DONE, 1u) + 1 == P.nruns ? 1u : 0u;
+  }
+  __syncthreads();
+  if (L.act) finish_call<G>(P, L, tid0);
 }
 
 // The next run or piece after flat index r with an entry (lane 0; every
@@ -2033,7 +2091,7 @@ XYWS_DEV void chain_start(lds_t<G>& L, const cstate& S, uint64_t hn, uint64_t Wn
 // Walk the runs from run 0 along their successors, repairing every boundary
 // whose chain did not land on the successor's entry, then the frame count, the
 // carry and the descriptor plan (one workgroup; every run has exited).
-// Serial walk with repairs (whole workgroup; k_stream_finish calls it when the
+// Serial walk with repairs (whole workgroup; finish_call runs it when the
 // fast path found a bad hand-over). Lane 0 keeps the current chain piece in
 // L.wk: the run whose descriptor plan it fills (r, efrom, ecarry), its frames
 // (cnt; tail = those past the successor's entry), its final state F, its
@@ -2150,27 +2208,47 @@ XYWS_DEV void finish_walk(const run_params& P, lds_t<G>& L, uint32_t tid) {
 // Walk the runs from run 0 along their successors, repairing every boundary
 // whose chain did not land on the successor's entry, then the frame count, the
 // carry and the descriptor plan (one workgroup; every run has exited).
+// Run by the workgroup whose done-count add came last (every other workgroup
+// has written its records and exited). When every hand-over was good and no
+// descriptors are asked for, the call's outputs come from the end-of-call
+// words (the frame total, the final state): a few loads. Otherwise the run
+// records are scanned (finish_fast: total, carry, descriptor plan, bad
+// hand-overs) and bad hand-overs are repaired (finish_walk). Then the ticket,
+// the done count and the end-of-call words are reset and the epoch advances,
+// so the next call (or graph replay) starts clean without a memset.
+// (not inlined: the record scan and the repair walk stay out of the decode
+// loop's register allocation)
 template <class G>
-__global__ void __launch_bounds__(G::NT) k_stream_finish(run_params P) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
-  lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
-  const uint32_t tid = threadIdx.x;
-#if XYWS_EXP_FINISH == 2  // (timing experiment only: no fast path)
-  if (tid == 0) { L.E = st_load(reinterpret_cast<const uint64_t*>(P.head + HEAD_EPOCH)) + 1; L.act = 0; L.aux2 = 0; }
-  __syncthreads();
-#else
-  finish_fast<G>(P, L, tid);
-#endif
-  const uint64_t E = L.E;
-#if XYWS_EXP_FINISH == 0
-  if (L.act) finish_walk<G>(P, L, tid);
-#endif
+__device__ __attribute__((noinline)) void finish_call(run_params P, lds_t<G>& L, uint32_t tid) {
+  uint64_t* hw = reinterpret_cast<uint64_t*>(P.head);
   if (tid == 0) {
-    if (XYWS_EXP_FINISH != 4) write_outputs(P, &L.cinc, L.aux2, L.S);
-    // every run has exited: the ticket starts the next call at zero; the
-    // epoch word advances (this call's entry granules read as stale from now on)
-    P.head[0] = 0;
-    st_store(reinterpret_cast<uint64_t*>(P.head + HEAD_EPOCH), E);
+    const uint64_t bad = st_load(hw + HW_BAD);
+    L.act = (bad || (P.frames && P.cap)) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (L.act) {
+    finish_fast<G>(P, L, tid);
+    if (L.act) finish_walk<G>(P, L, tid);
+    if (tid == 0) write_outputs(P, &L.cinc, L.aux2, L.S);
+  } else if (tid == 0) {
+    // (all loads first: one memory round trip)
+    uint64_t c[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) c[i] = st_load(reinterpret_cast<const uint64_t*>(P.cin) + i);
+    const uint64_t total = st_load(hw + HW_TOTAL);
+    const cstate S = get_state(hw + HW_FINAL);
+#pragma unroll
+    for (int i = 0; i < 8; i++) reinterpret_cast<uint64_t*>(&L.cinc)[i] = c[i];
+    write_outputs(P, &L.cinc, total, S);
+  }
+  if (tid == 0) {
+    st_store(hw + HW_BAD, 0);
+    st_store(hw + HW_TOTAL, 0);
+    st_store(hw + HW_DONE, 0);
+    // the ticket starts the next call at zero; the epoch word advances (this
+    // call's entry granules read as stale from now on)
+    __hip_atomic_store(P.head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_store(reinterpret_cast<uint64_t*>(P.head + HEAD_EPOCH), L.E);
   }
 }
 
@@ -2234,7 +2312,8 @@ __global__ void k_stream_empty(const xyws_carry* cin, xyws_carry* cout, uint64_t
   }
 }
 
-constexpr uint64_t HEAD_BYTES = 512;  // [0] ticket, [1] error, [2..3] total, [4..5] epoch; [64..128) carry; [128..512) stats
+constexpr uint64_t HEAD_BYTES = 1024;  // u32 [0] ticket, [1] error, [2..3] total, [4..5] epoch; bytes [64..128) carry,
+                                       // [128..512) stats, [512..576) end-of-call words (HW_*)
 
 // hipFuncSetAttribute applies to the current device: once per (device,
 // geometry), under a lock (one process may drive several devices from several
@@ -2249,9 +2328,7 @@ int set_lds_attr() {
   if (done[dev]) return XYWS_OK;
   const int lds = (int)sizeof(lds_t<G>);
   if (hipFuncSetAttribute((const void*)k_stream_runs<G>, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
-          hipSuccess ||
-      hipFuncSetAttribute((const void*)k_stream_finish<G>, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
-          hipSuccess)
+      hipSuccess)
     return XYWS_ERR_HIP;
   done[dev] = true;
   return XYWS_OK;
@@ -2262,7 +2339,6 @@ int launch_runs(const run_params& P, hipStream_t stream) {
   const size_t lds = sizeof(lds_t<G>);
   if (const int rc = set_lds_attr<G>()) return rc;
   hipLaunchKernelGGL(k_stream_runs<G>, dim3(P.nruns), dim3(G::NT), lds, stream, P);
-  hipLaunchKernelGGL(k_stream_finish<G>, dim3(1), dim3(G::NT), lds, stream, P);
   if (P.frames && P.cap) hipLaunchKernelGGL(k_stream_emit, dim3(P.nflat), dim3(64), 0, stream, P);
   return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
@@ -2386,7 +2462,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   P.prog = reinterpret_cast<uint64_t*>(m + HEAD_BYTES + granules_bytes(s->max_runs) + split_bytes(s->max_runs));
   P.rec = reinterpret_cast<uint64_t*>(m + records_off(s->max_runs));
   P.opts = opts;
-  // The ticket is zero here (zeroed at allocation, reset by k_stream_finish
+  // The ticket is zero here (zeroed at allocation, reset by finish_call
   // after every call); granules, split and progress words carry the epoch of
   // the call that wrote them; the error word [1] is sticky until read back.
   // Run 0 snapshots the incoming carry into scratch.
