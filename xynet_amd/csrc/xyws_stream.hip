@@ -61,10 +61,6 @@ namespace {
 
 
 
-#ifndef XYWS_EXP_NODMA
-#define XYWS_EXP_NODMA 0  // timing experiments (scripts/exp_variants.sh): 1 = first segment through registers
-#endif
-
 constexpr uint64_t NONE = ~0ull;
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr uint32_t PAD = 32;          // LDS bytes after the segment (5-dword header reads)
@@ -202,8 +198,8 @@ XYWS_DEV void granule_load(const uint64_t* g, uint64_t& a, uint64_t& b) {
 //   ACC    the run agrees, the piece starts at segment e',
 //   CLS    the run will not split (no entry, too little left, successor
 //          already looked up, or a refused request).
-// The run reads its split word with one LDS-DMA load per segment (issued
-// before the prefetch, so the fill's wait covers it: no stall, no register).
+// The run reads its split word with one load per segment (lane 0, issued
+// before the prefetch and used one iteration later: no stall).
 enum { SP_FREE = 0, SP_REQ = 1, SP_ACC = 2, SP_CLS = 3 };
 XYWS_DEV uint64_t split_word(uint64_t E, uint32_t state, uint32_t e) {
   return (E << 24) | ((uint64_t)state << 22) | (e & 0x3FFFFFu);
@@ -253,7 +249,7 @@ struct __attribute__((aligned(16))) lds_t {
   uint64_t rng_end;    // end of the current run's range (a run's shrinks when a thief takes its tail)
   uint64_t rs;         // start of the current run's range (segment grid of the split word)
   uint64_t split_e;    // own run: first segment of the piece taken from it (NONE: none)
-  uint64_t split_poll[2] __attribute__((aligned(16)));  // LDS-DMA target: the run's split word
+  uint64_t split_poll[2] __attribute__((aligned(16)));  // the run's split word at the start of an item
   uint64_t self;       // flat index of the run or piece being decoded
   uint32_t victim;     // 1: the current run answers steal requests (an own run, not yet closed)
   walk_t wk;       // finish_call: the current chain piece
@@ -498,40 +494,6 @@ struct seg_io {
     for (uint32_t k = 0; k < G::CH; k++)
       e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16u, k * G::NT * 16u, AUX_NT);
     pf = ss;
-  }
-  // A run's first segment straight into LDS (LDS-DMA, 16 bytes per lane, the
-  // same chunk layout as fill) and the next segment's loads into the registers
-  // behind it, both in flight at once: the first segment is scanned while the
-  // second one streams in. The DMA loads are invisible to the compiler (asm:
-  // no implicit wait for them before the LDS reads, which would also wait for
-  // the prefetch); the explicit vmcnt(CH) leaves only the prefetch in flight
-  // (vector memory ops complete in issue order). Caller syncs after.
-  XYWS_DEV void fill_dma_and_issue(const run_params& P, lds_t<G>& L, uint64_t ss_in, uint32_t tid) {
-    const uint64_t ss = uniform64(ss_in);
-    // the buffer descriptor of seg_rsrc as four SGPRs (words readfirstlane'd:
-    // the asm operand must be scalar)
-    uint64_t top = (P.hi + 15) & ~15ull;
-    const uint64_t room = top > ss ? top - ss : 0;
-    const uint64_t a = (uint64_t)(uintptr_t)(P.base + ss);
-    u32x4 rs;
-    rs.x = __builtin_amdgcn_readfirstlane((uint32_t)a);
-    rs.y = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xFFFFu);
-    rs.z = __builtin_amdgcn_readfirstlane(room >= G::SEG ? G::SEG : (uint32_t)room);
-    rs.w = 0x00020000u;
-    const uint32_t wave_lds = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)&L.seg[(tid & ~63u) * 16u]);
-#pragma unroll
-    for (uint32_t k = 0; k < G::CH; k++) {
-      asm volatile("s_mov_b32 m0, %1\n\tbuffer_load_dwordx4 %0, %2, %3 offen nt lds"
-                   :: "v"(tid * 16u), "s"(wave_lds + k * G::NT * 16u), "s"(rs), "s"(k * G::NT * 16u)
-                   : "memory", "m0");
-    }
-    const bool more = ss + G::SEG < P.hi;
-    if (more) issue(P, ss + G::SEG, tid);
-    if (more)
-      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(G::CH) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   // the segment at ss into LDS (caller syncs before and after)
   XYWS_DEV void fill(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid) {
@@ -1035,13 +997,12 @@ XYWS_DEV void close_split(const run_params& P, uint64_t* sw, uint64_t E) {
   if (old != fr && split_is(old, E, SP_REQ)) st_store(sw, split_word(E, SP_CLS, 0));
 }
 
-// A steal request seen in the split word the run DMA'd into LDS (lane 0, at
-// the top of the segment at ss, after the fill's wait covered that load): the
+// A steal request seen in the split word w the run loaded one segment earlier
+// (lane 0, at the top of the segment at ss): the
 // run keeps the current and the next segment and about half of the rest
 // (less one segment, the thief's entry scan), the thief gets the tail.
 template <class G>
-XYWS_DEV void answer_split(const run_params& P, lds_t<G>& L, uint64_t ss) {
-  const uint64_t w = L.split_poll[0];
+XYWS_DEV void answer_split(const run_params& P, lds_t<G>& L, uint64_t ss, uint64_t w) {
   if (!split_is(w, L.E, SP_REQ)) return;
   uint64_t* sw = P.split + 2 * (L.self >> 1);
   const uint64_t rend = L.rng_end < P.hi ? L.rng_end : P.hi;
@@ -1114,6 +1075,7 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
     }
   };
   lookup(ss0 + G::SEG);
+  uint64_t split_w = L.split_poll[0];  // the run's split word as last read (lane 0)
   for (uint64_t ss = ss0;; ss += G::SEG) {
     const uint64_t nx = ss + G::SEG;
     __syncthreads();  // the previous segment's LDS reads are done; L control words visible
@@ -1124,11 +1086,10 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
       for (uint32_t k = 0; k < G::CH; k++)
         *reinterpret_cast<u32x4*>(&L.seg[(k * G::NT + tid) * 16u]) = io.e[k];
       io.pf = NONE;
-      // (wave 0's fill waited for its loads, among them lane 0's split-word
-      // DMA, issued before them; the prefetch registers are free here: the
-      // lane-0 work of a run that can be split goes where they are dead)
+      // (the prefetch registers are free here: the lane-0 work of a run that
+      // can be split goes where they are dead)
       asm volatile("" ::: "memory");
-      if (tid == 0 && L.victim) answer_split<G>(P, L, ss);
+      if (tid == 0 && L.victim) answer_split<G>(P, L, ss, split_w);
     }
     __syncthreads();
     XYWS_STAMP(acc_fill);
@@ -1138,12 +1099,14 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
     const bool fin0 = (L.end || L.done) && nx >= whi;
     const bool pf = nx < P.hi && nx < wlim && !fin0 && io.pf != nx;
     if (tid == 0 && L.victim && filled) {
-      // progress for thieves, and the split word into LDS for the next
-      // iteration (both before the prefetch: the next fill's wait covers them)
+      // progress for thieves, and the split word for the next iteration
+      // (both before the prefetch)
       const uint32_t r = (uint32_t)(L.self >> 1);
       st_store(P.prog + r, (L.E << 24) | ((ss - L.rs) / G::SEG));
-      __builtin_amdgcn_global_load_lds((const void*)(P.split + 2 * r),
-                                       (__attribute__((address_space(3))) void*)L.split_poll, 16, 0, 16);
+      // (a plain load into a register: the compiler waits for it where it is
+      // used, next iteration, by counting; an LDS-DMA here made it wait
+      // vmcnt(0), i.e. for the whole prefetch, at the next barrier)
+      split_w = st_load(P.split + 2 * r);
     }
     // (issuing each chunk's next load right after its LDS write made hipcc wait
     // for the new loads inside the fill: the prefetch goes after the barrier)
@@ -1184,6 +1147,11 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
         }
       }
       XYWS_STAMP(acc_cp);
+      // Large frames (serial chase): the next segment's loads and this run's
+      // earlier stores drain before this segment's stores go out (measured
+      // ~0.6 % faster on c3 than letting them overlap); the dense pass never
+      // waits here (its chase is what the prefetch hides).
+      if (!dense) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       XYWS_STAMP(acc_sync);
       const uint32_t nfl = L.nfl, hi_c = L.pass_hi;
@@ -1538,8 +1506,7 @@ XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32
   uint64_t tp = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
   for (uint64_t ss = rb; ss < re; ss += G::SEG) {
     __syncthreads();
-    if (!XYWS_EXP_NODMA && io.pf == NONE && !(P.opts & XYWS_OPT_DIAG)) io.fill_dma_and_issue(P, L, ss, tid);
-    else io.fill(P, L, ss, tid);
+    io.fill(P, L, ss, tid);
     if (tid == 0) { L.best = 0xFFFFFFFFu; L.aux1 = ss; }
     __syncthreads();
     if (stats_on(P) && tid == 0) {
@@ -1551,7 +1518,7 @@ XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32
     // the entry is in this segment, the scan continues there when it is not
     // (HBM would idle during the scan otherwise; the few header reads from
     // memory below and the publish's vmcnt(0) wait for them)
-    if (ss + G::SEG < P.hi && !(P.opts & XYWS_OPT_DIAG) && io.pf != ss + G::SEG) io.issue(P, ss + G::SEG, tid);
+    if (ss + G::SEG < P.hi && !(P.opts & XYWS_OPT_DIAG)) io.issue(P, ss + G::SEG, tid);
     scan_segment<G>(P, L, ss, tid, unm);
     if (stats_on(P) && tid == 0) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
