@@ -196,7 +196,11 @@ int xyws_decode_stream(xyws_ctx* ctx, void* dev_buf, uint64_t len,
  * (:378-384). The bytes are parsed on the device by the stream decoder in
  * parse-only mode with a device-resident carry; parse() is synchronous on
  * `stream` (it returns the reference's answer). result() before a header
- * completed returns zero flags, key and length. */
+ * completed returns what the reference's state machine holds at that point
+ * (:305-385): flags from the first byte, HAS_MASK and the 7-bit length from
+ * the second (0 for the 126/127 forms), the extended length accumulated over
+ * the bytes received, the mask bytes received so far (checked against the
+ * reference's parser corpus, tests/golden/parse_corpus.json). */
 typedef struct xyws_parser xyws_parser;
 int xyws_parser_create(xyws_ctx* ctx, xyws_parser** out);
 int xyws_parser_destroy(xyws_parser* p);

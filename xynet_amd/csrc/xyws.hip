@@ -485,14 +485,38 @@ int xyws_decode_stream(xyws_ctx* ctx, void* dev_buf, uint64_t len, const xyws_ca
 // header byte, so the bytes consumed in the completing call are its hdr_len
 // minus the bytes fed before it (:342, :362, :375); once complete, parse()
 // returns npos until reset() (:378-384).
+// While a header is incomplete, result() reports what the reference's state
+// machine has parsed so far (:305-385): flags from the first byte (FIN, opcode),
+// HAS_MASK and the 7-bit length from the second (0 for the 126/127 forms), the
+// extended length accumulated big-endian over the bytes received, the mask
+// bytes received so far; partial_result() computes that from the header bytes
+// fed since reset() (at most 13), which parse() keeps on the host.
 struct xyws_parser {
   xyws_ctx* ctx;
   uint8_t* dev;       // device: carry (64 B) | frame (32 B) | count (8 B) | staging (32 B)
-  uint8_t* host;      // pinned: frame (32 B) | count (8 B)
+  uint8_t* host;      // pinned: frame (32 B) | count (8 B) | input header bytes (16 B at +48)
   uint64_t fed;       // header bytes fed since reset()
+  uint8_t hb[XYWS_MAX_FRAME_HEADER_SIZE];  // those bytes
   bool finished;
   xyws_frame res;
 };
+
+static void partial_result(const uint8_t* hb, uint64_t k, xyws_frame* r) {
+  memset(r, 0, sizeof *r);  // reset(): no flags, zero mask, zero length
+  if (k == 0) return;
+  r->flags = (uint8_t)((hb[0] & 0x0Fu) | ((hb[0] & 0x80u) ? XYWS_FLAG_FIN : 0u));
+  if (k == 1) return;
+  uint64_t len = hb[1] & 0x7Fu;
+  if (hb[1] & 0x80u) r->flags |= XYWS_FLAG_HAS_MASK;
+  const uint64_t ext = len == 127 ? 8 : len == 126 ? 2 : 0;
+  if (ext) {
+    len = 0;
+    for (uint64_t i = 2; i < 2 + ext && i < k; i++) len = (len << 8) | hb[i];
+  }
+  r->payload_len = len;
+  if (r->flags & XYWS_FLAG_HAS_MASK)
+    for (uint64_t i = 2 + ext; i < k && i < 2 + ext + 4; i++) r->key[i - 2 - ext] = hb[i];
+}
 
 int xyws_parser_create(xyws_ctx* ctx, xyws_parser** out) {
   if (!ctx || !out) return XYWS_ERR_INVALID;
@@ -557,6 +581,9 @@ int xyws_parser_parse(xyws_parser* p, const void* data, uint64_t len, uint64_t* 
   if (!on_dev) {
     if (hipMemcpyAsync(stage, data, n, hipMemcpyHostToDevice, s) != hipSuccess) return XYWS_ERR_HIP;
     src = stage;
+    memcpy(p->hb + p->fed, data, n);
+  } else if (hipMemcpyAsync(p->host + 48, data, n, hipMemcpyDeviceToHost, s) != hipSuccess) {
+    return XYWS_ERR_HIP;
   }
   int rc = xyws_decode_stream(p->ctx, const_cast<void*>(src), n, carry, carry, frame, 1, count,
                               XYWS_OPT_PARSE_ONLY, stream);
@@ -565,8 +592,10 @@ int xyws_parser_parse(xyws_parser* p, const void* data, uint64_t len, uint64_t* 
   if (hipStreamSynchronize(s) != hipSuccess) return XYWS_ERR_HIP;
   uint64_t nf;
   memcpy(&nf, p->host + 32, 8);
+  if (on_dev) memcpy(p->hb + p->fed, p->host + 48, n);
   if (nf == 0) {
     p->fed += n;
+    partial_result(p->hb, p->fed, &p->res);
     return XYWS_OK;
   }
   memcpy(&p->res, p->host, sizeof p->res);
