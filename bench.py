@@ -368,6 +368,8 @@ def main():
                     help="batch copies rotated over the steps (0: enough to exceed the 256 MiB Infinity Cache)")
     ap.add_argument("--dry-run", action="store_true", help="plan the N-rank run on the CPU (gloo) and exit")
     ap.add_argument("--stats", action="store_true", help="print fused-decoder resolution counters")
+    ap.add_argument("--frames", action="store_true",
+                    help="every step also returns the whole frame table and count (not the headline)")
     ap.add_argument("--xopts", type=lambda x: int(x, 0), default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -401,10 +403,23 @@ def main():
     dec.ctx.reserve(info["size"], 0)
     stream = torch.cuda.current_stream()
 
-    def step(i):  # fresh stream each step: no carry in/out, no frame table, no count
+    # --frames: every step also returns the whole frame table and the count
+    # (what a websocket_recv_data caller consumes), into buffers allocated once
+    frames_t = n_t = None
+    if args.frames:
+        frames_t = torch.empty(max(1, info["nframes"] + 2) * 32, dtype=torch.uint8, device="cuda")
+        n_t = torch.zeros(1, dtype=torch.int64, device="cuda")
+
+    def step(i):  # fresh stream each step: no carry in/out (no frame table, no count by default)
         k = i % ncopies
         uses[k] += 1
-        dec.decode(bufs[k], cap=0, count=False, carry=False)
+        if frames_t is None:
+            dec.decode(bufs[k], cap=0, count=False, carry=False)
+            return
+        rc = dec.ctx.L.xyws_decode_stream(dec.ctx.h, C.c_void_p(bufs[k].data_ptr()), bufs[k].numel(), None, None,
+                                          C.c_void_p(frames_t.data_ptr()), info["nframes"] + 2,
+                                          C.c_void_p(n_t.data_ptr()), dec.opts, C.c_void_p(stream.cuda_stream))
+        assert rc == 0, rc
 
     for i in range(args.warmup):
         step(i)
@@ -460,6 +475,8 @@ def main():
         parity = dev_err == 0
         for b, u in zip(bufs, uses):
             parity = parity and device_digest(torch, T, b) == (golden["out_digest"] if u % 2 else golden["in_digest"])
+        if n_t is not None:  # the count the frame-table steps returned
+            parity = parity and int(n_t.item()) == golden["decoded_frames"]
 
     per_gpu = args.steps * info["payload_bytes"] / t_own / GIB
     per_gpu_all = [per_gpu]
@@ -468,7 +485,8 @@ def main():
         dist.all_gather_object(per_gpu_all, round(per_gpu, 3))
     total_payload = info["payload_bytes"] * world
     value = args.steps * total_payload / elapsed / GIB
-    achieved = info["algo_bytes"] / (avg_ms * 1e-3) / 1e9
+    algo_bytes = info["algo_bytes"] + (32 * info["nframes"] if args.frames else 0)  # + the descriptors
+    achieved = algo_bytes / (avg_ms * 1e-3) / 1e9
     parity_all = all_ranks(dist, torch, parity, "cuda") if dist else parity
 
     cpu = None
@@ -485,7 +503,7 @@ def main():
             host_rate = host_path_rate(torch, ws, T, info, bufs[0], golden)
             host_rate["arena"] = arena_path_rate(torch, ws, T, info, bufs[0], golden)
 
-    traffic, traffic_src = pmc_traffic(args.config, args.mode)
+    traffic, traffic_src = pmc_traffic(args.config, args.mode + ("+frames" if args.frames else ""))
 
     if rank == 0:
         line = {
@@ -503,7 +521,8 @@ def main():
             "data": "synthetic (splitmix64 masked frames generated in HBM; include/xyws_synth.h)",
             "config": {
                 "workload": info["desc"],
-                "mode": args.mode + " (xyws_decode_stream: boundaries discovered on device)",
+                "mode": args.mode + " (xyws_decode_stream: boundaries discovered on device)" +
+                        (", whole frame table + count returned every step" if args.frames else ""),
                 "frames_per_gpu": info["nframes"],
                 "batch_bytes_per_gpu": info["size"],
                 "payload_bytes_per_gpu": info["payload_bytes"],
@@ -519,7 +538,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": info["algo_bytes"],
+                "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_ms_avg": round(avg_ms, 4),
                 "kernel_ms_note": "HIP-event time per decode over the timed steps (runs + finish kernels "
                                   "and the gaps between steps); per-kernel split: profiles/*_kernel_stats.csv",

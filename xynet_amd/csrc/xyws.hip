@@ -347,6 +347,10 @@ int xyws_ctx_reserve(xyws_ctx* ctx, uint64_t max_batch_bytes, uint64_t max_frame
     }
     int rc = stream_scratch_reserve(&sl.ss, ctx->reserve_bytes);
     if (rc) return rc;
+    if (ctx->reserve_frames) {
+      rc = stream_scratch_reserve_frames(&sl.ss, ctx->reserve_bytes, ctx->reserve_frames);
+      if (rc) return rc;
+    }
   }
   return XYWS_OK;
 }

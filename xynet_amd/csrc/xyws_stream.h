@@ -11,11 +11,14 @@ struct stream_scratch {
   uint64_t bytes;
   uint64_t max_runs;    // runs the allocation covers
   int ncu;              // compute units of the context's device (runs per launch)
+  void* fmem;           // frame-start lists for descriptor emission (grown with the caller's cap)
+  uint64_t fbytes;
 };
 
 void stream_scratch_init(stream_scratch* s, int device);
 void stream_scratch_free(stream_scratch* s);
 int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes);
+int stream_scratch_reserve_frames(stream_scratch* s, uint64_t max_batch_bytes, uint64_t max_frames);
 // sticky device error word of this scratch (bit 1: an inter-workgroup wait
 // timed out, bit 2: a run record was not written by its call); clear: reset
 // it after reading (the device must be idle)

@@ -144,6 +144,7 @@ enum {
   R_T0, R_T1, R_T2,                                 // stats mode: s_memrealtime at start, after the prologue, at the end
   R_SPLIT,                                          // own runs: the split segment a thief took the rest from (NONE: none)
   R_XCC,                                            // stats mode: the XCD (XCC_ID) the run's workgroup ran on
+  R_NREC,                                           // descriptors requested: frame starts in the item's region
   R_WORDS = 32
 };
 // R_OK bits
@@ -173,6 +174,12 @@ constexpr uint32_t HEAD_EPOCH = 4;   // u32 index of the u64 epoch word in head[
 // done, hand-overs that need the repair walk, frames of all items, and the
 // final chain state of the item whose chain reached the batch end.
 constexpr uint32_t HW_DONE = 64, HW_BAD = 65, HW_TOTAL = 66, HW_FINAL = 67;
+// descriptor emission: non-zero when the frame-start lists cannot be used (a
+// region overflowed, or a repaired hand-over changed the plan) and
+// k_stream_emit re-walks the chains instead
+constexpr uint32_t HW_EMIT_SLOW = 73;
+// ...copied by finish_call for k_stream_emit (and reset there)
+constexpr uint32_t HW_EMIT_FLAG = 74;
 
 XYWS_DEV void granule_store(uint64_t* g, uint64_t a, uint64_t b) {
   const u32x4 v = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
@@ -227,6 +234,11 @@ struct run_params {
   uint32_t* head;         // [0] ticket, [1] error word, [2..3] u64 total, [4..5] u64 epoch;
                           // [16..32) carry snapshot; stats at [32..)
   uint32_t opts;
+  // descriptors requested: the starts of the frames each item (run or piece)
+  // finds, in chain order, in its own region of rcap entries (fst + item *
+  // rcap); k_stream_emit writes the descriptors from them in parallel
+  uint64_t* fst;
+  uint64_t rcap;
 };
 
 template <class G>
@@ -264,6 +276,7 @@ struct __attribute__((aligned(16))) lds_t {
   uint32_t dent[G::NSB], dcnt[G::NSB], dexit[G::NSB], doff[G::NSB];
   uint4 dlast[G::NSB];
   uint32_t dense;  // frames of the previous pass (the dense pass is tried after a dense one)
+  uint32_t nrec;   // descriptors requested: frame starts the current item recorded
 };
 
 // ---------------------------------------------------------------- small helpers
@@ -565,6 +578,33 @@ XYWS_DEV bool parse_rel(const lds_t<G>& L, uint32_t x, uint32_t& hl, uint32_t& p
   return true;
 }
 
+// Descriptors requested (lane 0): the k frames starting at frame-list entry
+// `first` (segment-relative starts), the item's own frames found by this pass,
+// appended to the item's region. An overflow switches the emission to the
+// chain re-walk.
+XYWS_DEV void flag_emit_slow(const run_params& P) {
+  __hip_atomic_fetch_or(reinterpret_cast<uint64_t*>(P.head) + HW_EMIT_SLOW, 1ull, __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class G>
+XYWS_DEV void record_starts(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t first, uint32_t k) {
+  if (!P.fst || !k) return;
+  const uint64_t n = L.nrec;
+  if (n + k > P.rcap) { flag_emit_slow(P); return; }
+  uint64_t* dst = P.fst + L.self * P.rcap + n;
+#pragma unroll 1
+  for (uint32_t i = 0; i < k; i++) dst[i] = ss + L.fl[first + i].start;
+  L.nrec = (uint32_t)(n + k);
+}
+// one frame start (absolute): the prologue's head frames
+template <class G>
+XYWS_DEV void record_start(const run_params& P, lds_t<G>& L, uint64_t self, uint64_t x) {
+  if (!P.fst) return;
+  if (L.nrec + 1 > P.rcap) { flag_emit_slow(P); return; }
+  P.fst[self * P.rcap + L.nrec] = x;
+  L.nrec++;
+}
+
 // One pass of the chase over segment [ss, ss+SEG), lane 0: the frame covering
 // the pass start, then frames parsed from X, up to G::FCAP entries. Sets
 // pass_hi: the chunks below it are final for this pass.
@@ -585,6 +625,7 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   const uint64_t lim = known ? L.Wn : NONE, hn = L.hn;
   bool past = L.past != 0, done = false, end = false;
   uint64_t cnt = 0, tail = 0;
+  const uint32_t first_new = n;  // (the own frames of this pass come first, then any past the successor's entry)
   for (;;) {
     {
       // Fast path (many frames per segment): 32-bit segment-relative parse of
@@ -655,6 +696,7 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   L.S = S;
   L.nfl = n;
   L.dense = n;
+  if (P.fst) record_starts<G>(P, L, ss, first_new, (uint32_t)cnt);
   const bool seg_done = S.X >= se || end || done;
   L.pass_hi = seg_done ? G::SEG : (uint32_t)((S.X - ss) & ~15ull);
 }
@@ -839,13 +881,22 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   }
   const uint32_t total = L.ccnt;
   if (total == NONE32) return false;
-  // 4. compaction (each thread moves at most one entry) and the chain state
+  // 4. compaction (each thread moves at most one entry) and the chain state;
+  //    descriptors requested: each thread also records its frame's start in
+  //    the item's region (own frames only; the list is full: the re-walk)
+  const uint32_t c0 = cover ? 1u : 0u, frames = total - c0;
+  const bool rec_ok = P.fst && !past && L.nrec + frames <= P.rcap;
   {
     const uint32_t s = tid / SECT, j = tid % SECT, skip = L.dent[s];
     const bool mv = j >= skip && j < L.dcnt[s];
     const u32x4 e = mv ? *reinterpret_cast<const u32x4*>(&L.fl[tid]) : u32x4{0u, 0u, 0u, 0u};
+    const uint64_t rbase = L.self * P.rcap + L.nrec;
     __syncthreads();
-    if (mv) *reinterpret_cast<u32x4*>(&L.fl[L.doff[s] + j - skip]) = e;
+    if (mv) {
+      const uint32_t pos = L.doff[s] + j - skip;
+      *reinterpret_cast<u32x4*>(&L.fl[pos]) = e;
+      if (rec_ok) P.fst[rbase + pos - c0] = ss + e.x;
+    }
   }
   if (tid == 0) {
     if (cover) {
@@ -860,7 +911,6 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
     while (last > 0 && L.dcnt[last] == L.dent[last]) last--;
     const uint4 f = L.dlast[last];
     const uint32_t xe = L.dexit[NSB - 1];
-    const uint32_t frames = total - (cover ? 1u : 0u);
     if (frames) {
       cstate S;
       S.cov_start = ss + f.x; S.cov_ps = ss + f.y; S.X = ss + xe;
@@ -870,6 +920,8 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
     if (past) L.tail += frames; else L.cnt += frames;
     L.nfl = total;
     L.dense = total;
+    if (rec_ok) L.nrec += frames;
+    else if (P.fst && !past) flag_emit_slow(P);
     stat_add(P, ST_SEGS, 1);
     L.pass_hi = xe >= G::SEG ? G::SEG : (xe & ~15u);
   }
@@ -1560,9 +1612,11 @@ XYWS_DEV void prologue(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t
         // frames starting below W: parsed here, from bytes nobody writes yet
         S = frame_state(h, hh);
         hc = 1;
+        record_start<G>(P, L, self, h);
         while (S.X < W && S.X < P.hi) {
           const hdr_info hx = hdr_at(P, L, ss, S.X, NONE);
           if (!hx.hlen) { S.st |= S_PARTIAL; break; }
+          record_start<G>(P, L, self, S.X);
           S = frame_state(S.X, hx);
           hc++;
         }
@@ -1807,6 +1861,7 @@ XYWS_DEV void decode_range(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint
     st_store(rec + R_FIRST, L.first_after);
     put_state(rec + R_F0, L.S);
     st_store(rec + R_EP, L.E);
+    if (P.fst) st_store(rec + R_NREC, L.nrec);
     // what the workgroup finishing the call needs when every hand-over is
     // good: the frame total and the final state (the item without successor)
     uint64_t* hw = reinterpret_cast<uint64_t*>(P.head);
@@ -1970,6 +2025,7 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
     const uint64_t rng_end = re < P.hi ? re : NONE;
     uint64_t wlo = P.lo, ss0 = 0;
     bool in_lds = false, entry = true;
+    if (tid == 0) L.nrec = 0;  // (read by lane 0 after the barriers below)
     if (self != 0) {
       prologue<G>(P, L, io, tid, self, rb, re);
       entry = L.aux2 != NONE;  // (no entry: the chain of an earlier run covers this range)
@@ -2193,9 +2249,11 @@ __device__ __attribute__((noinline)) void finish_call(run_params P, lds_t<G>& L,
     L.act = (bad || (P.frames && P.cap)) ? 1u : 0u;
   }
   __syncthreads();
+  bool walked = false;
   if (L.act) {
     finish_fast<G>(P, L, tid);
-    if (L.act) finish_walk<G>(P, L, tid);
+    walked = L.act != 0;
+    if (walked) finish_walk<G>(P, L, tid);
     if (tid == 0) write_outputs(P, &L.cinc, L.aux2, L.S);
   } else if (tid == 0) {
     // (all loads first: one memory round trip)
@@ -2209,6 +2267,12 @@ __device__ __attribute__((noinline)) void finish_call(run_params P, lds_t<G>& L,
     write_outputs(P, &L.cinc, total, S);
   }
   if (tid == 0) {
+    if (P.fst) {
+      // the frame-start lists stand unless they overflowed or a repair changed
+      // the plan (k_stream_emit then re-walks the chains)
+      st_store(hw + HW_EMIT_FLAG, (walked || st_load(hw + HW_EMIT_SLOW)) ? 1u : 0u);
+      st_store(hw + HW_EMIT_SLOW, 0);
+    }
     st_store(hw + HW_BAD, 0);
     st_store(hw + HW_TOTAL, 0);
     st_store(hw + HW_DONE, 0);
@@ -2234,36 +2298,52 @@ XYWS_DEV void write_frame(const run_params& P, uint64_t ord, uint64_t start, con
   P.frames[ord] = f;
 }
 
-// Descriptors: one lane per run re-chases the run's frames (headers are never
-// modified by the decode) and writes them at their ordinals.
-__global__ void __launch_bounds__(64) k_stream_emit(run_params P) {
-  const uint32_t r = blockIdx.x;
-  if (threadIdx.x != 0 || r >= P.nflat) return;
+// Descriptors, one workgroup per run or piece at the ordinals finish_call
+// planned: the carried-header frame first (run 0), then the frame starts the
+// item recorded, in chain order, each header parsed from memory by its own lane (headers are never modified by the decode). When those lists are
+// unusable (HW_EMIT_FLAG) lane 0 re-chases the item's frames from its first one.
+__global__ void __launch_bounds__(256) k_stream_emit(run_params P) {
+  const uint32_t r = blockIdx.x, tid = threadIdx.x;
+  if (r >= P.nflat) return;
   const uint64_t* rec = P.rec + (uint64_t)r * R_WORDS;
-  uint64_t ord = st_load(rec + R_EORD);
+  const uint64_t ord = st_load(rec + R_EORD);
   const uint64_t n = st_load(rec + R_ECNT);
   if (n == 0 || ord >= P.cap) return;
   const uint64_t end = ord + n < P.cap ? ord + n : P.cap;
-  uint64_t X = st_load(rec + R_EFROM);
-  if (st_load(rec + R_ECARRY)) {  // run 0: the carried-header frame comes first
+  const bool ecarry = st_load(rec + R_ECARRY) != 0;
+  const bool slow = st_load(reinterpret_cast<const uint64_t*>(P.head) + HW_EMIT_FLAG) != 0;
+  uint64_t o = ord, X = st_load(rec + R_EFROM);
+  if (ecarry) {  // run 0: the carried-header frame comes first
     X = P.lo;
     if (!P.cin->payload_remaining && P.cin->hdr_len) {
       const hdr_info hh = header_carried(P, P.cin);
       if (hh.hlen) {
         const uint64_t ps = P.lo + (hh.hlen - P.cin->hdr_len);
-        write_frame(P, ord++, P.lo, hh, ps, (int32_t)P.cin->hdr_len);
+        if (tid == 0) write_frame(P, o, P.lo, hh, ps, (int32_t)P.cin->hdr_len);
+        o++;
         X = sat_add(ps, hh.plen);
       }
     } else if (P.cin->payload_remaining) {
       X = sat_add(P.lo, P.cin->payload_remaining);
     }
   }
-  while (ord < end && X < P.hi) {
-    const hdr_info hh = hdr_global(P, X, NONE);
-    if (!hh.hlen) break;
-    const uint64_t ps = X + hh.hlen;
-    write_frame(P, ord++, X, hh, ps, 0);
-    X = sat_add(ps, hh.plen);
+  if (slow) {
+    if (tid != 0) return;
+    while (o < end && X < P.hi) {
+      const hdr_info hh = hdr_global(P, X, NONE);
+      if (!hh.hlen) break;
+      const uint64_t ps = X + hh.hlen;
+      write_frame(P, o++, X, hh, ps, 0);
+      X = sat_add(ps, hh.plen);
+    }
+    return;
+  }
+  const uint64_t k = st_load(rec + R_NREC);
+  const uint64_t* src = P.fst + (uint64_t)r * P.rcap;
+  for (uint64_t i = tid; i < k && o + i < end; i += 256) {
+    const uint64_t x = src[i];
+    const hdr_info hh = hdr_global(P, x, NONE);
+    write_frame(P, o + i, x, hh, x + hh.hlen, 0);
   }
 }
 
@@ -2306,7 +2386,7 @@ int launch_runs(const run_params& P, hipStream_t stream) {
   const size_t lds = sizeof(lds_t<G>);
   if (const int rc = set_lds_attr<G>()) return rc;
   hipLaunchKernelGGL(k_stream_runs<G>, dim3(P.nruns), dim3(G::NT), lds, stream, P);
-  if (P.frames && P.cap) hipLaunchKernelGGL(k_stream_emit, dim3(P.nflat), dim3(64), 0, stream, P);
+  if (P.frames && P.cap) hipLaunchKernelGGL(k_stream_emit, dim3(P.nflat), dim3(256), 0, stream, P);
   return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
 
@@ -2316,6 +2396,8 @@ void stream_scratch_init(stream_scratch* s, int device) {
   s->mem = nullptr;
   s->bytes = 0;
   s->max_runs = 0;
+  s->fmem = nullptr;
+  s->fbytes = 0;
   s->ncu = 256;
   int n = 0;
   if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && n > 0)
@@ -2324,9 +2406,31 @@ void stream_scratch_init(stream_scratch* s, int device) {
 
 void stream_scratch_free(stream_scratch* s) {
   if (s->mem) (void)hipFree(s->mem);
+  if (s->fmem) (void)hipFree(s->fmem);
   s->mem = nullptr;
   s->bytes = 0;
   s->max_runs = 0;
+  s->fmem = nullptr;
+  s->fbytes = 0;
+}
+
+// Frame-start lists for descriptor emission: one region per flat item of
+// twice the caller's capacity spread over the runs + 1024 (a region that
+// overflows switches the call to the chain re-walk). Grown on demand, not
+// under graph capture (xyws_ctx_reserve).
+static uint64_t region_entries(uint64_t cap, uint64_t nruns) { return 2 * ((cap + nruns - 1) / nruns) + 1024; }
+static int fmem_grow(stream_scratch* s, uint64_t bytes, bool capturing) {
+  if (s->fmem && bytes <= s->fbytes) return XYWS_OK;
+  if (capturing) return XYWS_ERR_CAPACITY;
+  void* m = nullptr;
+  if (hipMalloc(&m, bytes) != hipSuccess) return XYWS_ERR_NOMEM;
+  if (s->fmem) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(s->fmem);
+  }
+  s->fmem = m;
+  s->fbytes = bytes;
+  return XYWS_OK;
 }
 
 // Scratch layout for up to `runs` runs (2 * runs flat indices):
@@ -2354,6 +2458,14 @@ static int scratch_grow(stream_scratch* s, uint64_t runs) {
   s->bytes = bytes;
   s->max_runs = want;
   return hipMemset(m, 0, records_off(want)) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
+}
+
+int stream_scratch_reserve_frames(stream_scratch* s, uint64_t max_batch_bytes, uint64_t max_frames) {
+  // the production geometry: one run per CU
+  const uint64_t runs = (uint64_t)s->ncu;
+  (void)max_batch_bytes;
+  const uint64_t nflat = 2 * runs;
+  return fmem_grow(s, 8 * nflat * region_entries(max_frames, runs), false);
 }
 
 int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
@@ -2436,6 +2548,14 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   if ((opts & XYWS_OPT_STATS) && hipMemsetAsync(m + 128, 0, 8 * XYWS_NSTATS, stream) != hipSuccess) return XYWS_ERR_HIP;
   P.cin_user = cin;
   P.cin = reinterpret_cast<xyws_carry*>(m + 64);
+  P.fst = nullptr; P.rcap = 0;
+  if (frames && cap) {
+    const uint64_t rc_n = region_entries(cap, nruns);
+    const int rc = fmem_grow(s, 8 * (uint64_t)P.nflat * rc_n, cs != hipStreamCaptureStatusNone);
+    if (rc) return rc;
+    P.fst = static_cast<uint64_t*>(s->fmem);
+    P.rcap = rc_n;
+  }
   return small ? launch_runs<G_SMALL>(P, stream)
                : wg512 ? launch_runs<G_PROD2>(P, stream) : launch_runs<G_PROD>(P, stream);
 }
