@@ -95,3 +95,32 @@ def test_wrong_hint_client_streams(ws, oracle, name):
     src = streams.case_bytes(name)
     for small_segments in (False, True):
         check_vs_oracle(ws, oracle, src, small_segments=small_segments, opts=OPT_UNMASKED_HINT)
+
+
+def test_descriptor_region_overflow_and_truncation(ws, oracle):
+    """Descriptor emission from the per-run frame-start regions: a run holding
+    far more frames than the batch average overflows its region (the call
+    falls back to re-walking the chains), and a caller capacity below the frame
+    count truncates the table; both must equal the oracle's descriptors."""
+    rng = streams.SplitMix(0xE417)
+    out = bytearray()
+    while len(out) < (48 << 20):  # large frames: few frames per run on average
+        plen = 60000 + rng.below(8000)
+        out += streams.header(0x82, plen, rng.bytes(4)) + rng.bytes(plen)
+    for _ in range(40000):        # one dense stretch (~320 KiB): thousands of frames in one run
+        plen = rng.below(2)
+        out += streams.header(0x82, plen, rng.bytes(4)) + rng.bytes(plen)
+    while len(out) < (64 << 20):
+        plen = 60000 + rng.below(8000)
+        out += streams.header(0x81, plen, rng.bytes(4)) + rng.bytes(plen)
+    src = bytes(out)
+    ob = np.frombuffer(src, np.uint8).copy()
+    ofr, carry, on = oracle.decode_stream(ob)
+    for cap in (on, on // 3):
+        view, _ = dev_bytes(src)
+        dec = ws.frame_decoder()
+        r = dec.decode(view, cap=cap)
+        assert r.nframes == on
+        assert host(view) == ob.tobytes()
+        assert frames_list(r.frames()[:cap], True) == frames_list(ofr[:cap], True)
+        assert dec.ctx.last_device_error() == 0
