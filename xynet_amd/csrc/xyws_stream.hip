@@ -2465,7 +2465,9 @@ int stream_scratch_reserve_frames(stream_scratch* s, uint64_t max_batch_bytes, u
   const uint64_t runs = (uint64_t)s->ncu;
   (void)max_batch_bytes;
   const uint64_t nflat = 2 * runs;
-  return fmem_grow(s, 8 * nflat * region_entries(max_frames, runs), false);
+  // (any smaller run count gives regions whose total is no larger, up to the
+  // rounding of cap / runs: + 4 entries per item)
+  return fmem_grow(s, 8 * nflat * (region_entries(max_frames, runs) + 4), false);
 }
 
 int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
