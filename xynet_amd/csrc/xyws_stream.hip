@@ -77,7 +77,11 @@ constexpr uint32_t PAD = 32;          // LDS bytes after the segment (5-dword he
 constexpr uint32_t KHDR_127 = 2, KHDR_126 = 6, KHDR_7 = 8;
 constexpr uint32_t SPIN = 1u << 24;   // bounded spins (s_sleep 2 each: ~1 s)
 constexpr uint32_t OOB = 0x80000000u; // buffer offset past every range: load 0, store dropped
-constexpr int AUX_NT = 2;             // buffer cache policy: nontemporal
+constexpr int AUX_NT = 2;             // buffer cache policy: nontemporal (the streaming loads)
+#ifndef XYWS_EXP_AUX_ST
+#define XYWS_EXP_AUX_ST 2
+#endif
+constexpr int AUX_ST = XYWS_EXP_AUX_ST;  // policy of the payload stores
 constexpr uint64_t PLEN_SPEC_MAX = 1ull << 46;
 constexpr uint32_t MAX_RUNS = 1024;
 // work stealing: a run is asked for its tail when it has at least this many
@@ -1037,7 +1041,7 @@ XYWS_DEV void dummy_stores(const run_params& P, uint64_t ss) {
   const __amdgpu_buffer_rsrc_t rz = seg_rsrc<G>(P, ss);
 #pragma unroll
   for (uint32_t k = 0; k < G::CH; k++)
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rz, OOB, k * G::NT * 16u, AUX_NT);  // distinct: not merged
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rz, OOB, k * G::NT * 16u, AUX_ST);  // distinct: not merged
 }
 
 // A run that will not split any more (lane 0; it is about to look up its
@@ -1268,7 +1272,7 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
           }
         }
         const u32x4 d = v ^ m;
-        __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, k * G::NT * 16u, AUX_NT);
+        __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, k * G::NT * 16u, AUX_ST);
         // hipcc (ROCm 7.2, gfx950) may overwrite a dwordx4 store's data VGPRs
         // in the very next instruction; later lanes then store the new value
         // (seen as wrong bytes in dword 0, lanes 12-15 of each 16). The data
@@ -1292,7 +1296,7 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
         if ((m.x | m.y | m.z | m.w) == 0u) continue;
         if (a >= wl_r && a + 16 <= wh_r) {
           const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
-          __builtin_amdgcn_raw_buffer_store_b128(v ^ m, rs, tid * 16u, k * G::NT * 16u, AUX_NT);
+          __builtin_amdgcn_raw_buffer_store_b128(v ^ m, rs, tid * 16u, k * G::NT * 16u, AUX_ST);
           asm volatile("s_nop 1" ::: "memory");
           continue;
         }
