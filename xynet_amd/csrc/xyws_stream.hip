@@ -706,7 +706,8 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
 }
 
 // Dense pass (many small frames): the segment's chase split over NSB
-// sub-blocks of SB bytes, four per wave, chased at once. Sub-block 0 starts
+// sub-blocks of SB bytes (entries searched by 16 lanes each, chased by one
+// lane each of wave 0), chased at once. Sub-block 0 starts
 // from the exact state; sub-block b > 0 from its speculated entry, the
 // earliest position in its first 512 bytes whose next 4 headers (32-bit parse
 // in LDS) have client first bytes. Every chase starts exactly where the previous
@@ -734,36 +735,37 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   __syncthreads();
   if (st_on) tq = __builtin_amdgcn_s_memtime();
   // 1. speculated entries: each lane of the 16-lane group takes WIN/16 bytes
+  //    and checks its candidates in order, one hop per loop iteration (a
+  //    single loop: the wave steps every lane's current chain together)
   if (sb > 0) {
     constexpr uint32_t WIN = SB < 512 ? SB : 512, PER = WIN / 16;
-    auto qchain = [&](uint32_t p) -> bool {
-      uint32_t x = p;
+    static_assert(PER == 16 || PER == 32, "entry window: one or two 16-byte chunks per lane");
+    const uint32_t a = sb * SB + gl * PER;
+    uint32_t bits = chunk_candidates<G>(P, L, a, unm);
+    if (PER == 32) bits |= chunk_candidates<G>(P, L, a + 16, unm) << 16;
+    uint32_t p = NONE32, x = 0, h = 0;
+    if (bits) { p = a + __builtin_ctz(bits); bits &= bits - 1; x = p; }
 #pragma unroll 1
-      for (uint32_t h = 0; h < 4; h++) {
-        if (x >= STOP) return h >= 3;  // (one long hop out of the segment proves little)
-        uint32_t hl, plen, key, b01;
-        if (!parse_rel<G>(L, x, hl, plen, key, b01)) return false;
-        if (!cand_pair(b01 & 0xFFu, b01 >> 8, unm)) return false;
+    while (p != NONE32) {
+      // 4 client headers in a row, or 3 and a hop out of the segment (one
+      // long hop proves little)
+      const bool in = x < STOP;
+      uint32_t hl = 0, plen = 0, key, b01;
+      const bool ok = in && parse_rel<G>(L, x, hl, plen, key, b01) && cand_pair(b01 & 0xFFu, b01 >> 8, unm);
+      if (in ? (ok && h == 3) : h >= 3) break;
+      if (ok) {
         x += hl + plen;
-      }
-      return true;
-    };
-#pragma unroll 1
-    for (uint32_t c = 0; c < PER / 16; c++) {
-      const uint32_t a = sb * SB + gl * PER + c * 16;
-      uint32_t bits = chunk_candidates<G>(P, L, a, unm);
-      bool hit = false;
-      while (bits) {
-        const uint32_t t = __builtin_ctz(bits);
+        h++;
+      } else if (bits) {
+        p = a + __builtin_ctz(bits);
         bits &= bits - 1;
-        if (qchain(a + t)) {
-          atomicMin(&L.dent[sb], a + t);
-          hit = true;
-          break;
-        }
+        x = p;
+        h = 0;
+      } else {
+        p = NONE32;
       }
-      if (hit) break;
     }
+    if (p != NONE32) atomicMin(&L.dent[sb], p);
   }
   __syncthreads();
   if (st_on) {
@@ -771,8 +773,11 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
     stat_add(P, ST_D_TENT, t - tq);
     tq = t;
   }
-  // 2. one chase per sub-block (lane 0 of each 16-lane group)
-  if (gl == 0) {
+  // 2. one chase per sub-block, all in wave 0 (lane b: sub-block b; one wave
+  //    stepping 64 chains issues a quarter of the instructions 16 waves
+  //    stepping 4 chains each do)
+  if (tid < NSB) {
+    const uint32_t sb = tid;
     uint32_t x = L.dent[sb], n = 0, lx = 0, lps = 0, lkey = 0, lkw = 0;
     bool fail = x == NONE32;
     const uint32_t end = (sb + 1) * SB;
