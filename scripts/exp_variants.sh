@@ -7,7 +7,7 @@ mode=$1; shift
 if [ "$mode" = build ]; then
   for v in "$@"; do
     name=${v%%:*}; flags=${v#*:}
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-function \
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -falign-loops=64 -std=c++17 -fPIC -shared -Wno-unused-function \
       -Iinclude -Ixynet_amd/csrc $flags xynet_amd/csrc/xyws.hip xynet_amd/csrc/xyws_stream.hip \
       xynet_amd/csrc/xyws_frames.hip xynet_amd/csrc/xyws_arena.hip -o exp/libxyws_$name.so || exit 1
   done

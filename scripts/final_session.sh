@@ -1,5 +1,5 @@
 set -e
-T=r02k
+T=${T:-r02k}
 TAG=$T scripts/gpu_session.sh tests smoke pmc:c3 pmc:c2 pmc:c1 pmc:c4
 for c in c3 c2 c1 c4; do python scripts/pmc_summary.py gpurun_out/${T}_pmc_${c}_fetch gpurun_out/${T}_pmc_${c}_write $c:fused ${T}_${c}_pmc; done
 cp profiles/pmc_traffic.json gpurun_out/${T}_pmc_traffic.json

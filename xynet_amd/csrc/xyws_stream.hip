@@ -110,7 +110,7 @@ struct geom {
   // frame-list entries per pass (one per thread: the dense pass compacts them
   // one per thread); prologue lists overlaying the frame list
   static constexpr uint32_t FCAP = NT_, SCAP = NT_ * 2, UCAP = NT_ * 2;
-  // dense pass: sub-blocks (four per wave), their bytes and list sections
+  // dense pass: sub-blocks (entries: 16 lanes each), their bytes and list sections
   static constexpr uint32_t NSB = NT_ / 16, SB = SEG / NSB, SECT = FCAP / NSB;
 };
 using G_PROD = geom<1024, 8, 4>;  // 128 KiB segments, 16 waves, one workgroup per CU (default)
@@ -717,9 +717,11 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
 // start is, by induction from sub-block 0. Entries go to per-sub-block sections
 // of the frame list and are compacted (one per thread). A last header that
 // does not fit the segment ends the pass (pass_hi) and the serial chase
-// continues it. Called only where no limit lies in the segment.
+// continues it; so does the serial chase from dstop, the successor's entry
+// when it lies in the segment (no write limit lies below it).
 template <class G>
-XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid_in, bool unm, bool past) {
+XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid_in, bool unm, bool past,
+                         uint32_t dstop) {
   // (the lane index made opaque here: its LDS address math is recomputed per
   // pass instead of being hoisted out of the segment loop and spilled)
   uint32_t tid = tid_in;
@@ -729,6 +731,8 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   const uint32_t lane = tid & 63u, gl = lane & 15u, sb = (tid >> 6) * 4 + (lane >> 4);
   const cstate S0 = L.S;
   const uint32_t x0 = (uint32_t)(S0.X - ss);
+  // sub-blocks starting below dstop (the successor's entry, or STOP) are chased
+  const uint32_t nact = (dstop + SB - 1) / SB;
   const bool st_on = stats_on(P) && tid == 0;
   uint64_t tq = st_on ? __builtin_amdgcn_s_memtime() : 0;
   if (gl == 0) L.dent[sb] = sb == 0 ? x0 : NONE32;
@@ -737,7 +741,7 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   // 1. speculated entries: each lane of the 16-lane group takes WIN/16 bytes
   //    and checks its candidates in order, one hop per loop iteration (a
   //    single loop: the wave steps every lane's current chain together)
-  if (sb > 0) {
+  if (sb > 0 && sb < nact) {
     constexpr uint32_t WIN = SB < 512 ? SB : 512, PER = WIN / 16;
     static_assert(PER == 16 || PER == 32, "entry window: one or two 16-byte chunks per lane");
     const uint32_t a = sb * SB + gl * PER;
@@ -776,12 +780,13 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   // 2. one chase per sub-block, all in wave 0 (lane b: sub-block b; one wave
   //    stepping 64 chains issues a quarter of the instructions 16 waves
   //    stepping 4 chains each do)
-  if (tid < NSB) {
+  if (tid < NSB && tid >= nact) L.dcnt[tid] = 0;
+  if (tid < nact) {
     const uint32_t sb = tid;
     uint32_t x = L.dent[sb], n = 0, lx = 0, lps = 0, lkey = 0, lkw = 0;
     bool fail = x == NONE32;
     const uint32_t end = (sb + 1) * SB;
-    while (!fail && x < end && x < STOP) {
+    while (!fail && x < end && x < dstop) {
       uint32_t hl, plen, key, b01;
       if (n >= SECT || !parse_rel<G>(L, x, hl, plen, key, b01)) { fail = true; break; }
       const uint32_t ps = x + hl, kw = rotr8(key, 0u - ps);
@@ -792,9 +797,9 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
       lx = x; lps = ps; lkey = key; lkw = kw;
       x = ps + plen;
     }
-    // (a header starting at or past STOP ends the pass; only the last
-    // sub-block can reach it)
-    if (x < end && sb + 1 < NSB) fail = true;
+    // (a header starting at or past dstop ends the pass; only the last
+    // chased sub-block can reach it)
+    if (x < end && sb + 1 < nact) fail = true;
     L.dcnt[sb] = fail ? NONE32 : n;
     L.dexit[sb] = x;
     L.dlast[sb] = uint4{lx, lps, lkey, lkw};
@@ -810,7 +815,7 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   if (tid < 64) {
     bool ok = true;
     uint32_t c = 0;
-    if (lane < NSB) {
+    if (lane < nact) {
       c = L.dcnt[lane];
       if (c == NONE32) {
         ok = false;
@@ -850,7 +855,7 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
       uint32_t tot = cover ? 1u : 0u;
       bool good = L.dcnt[0] != NONE32;
       if (good) { L.dent[0] = 0; L.doff[0] = tot; tot += L.dcnt[0]; }
-      for (uint32_t b = 1; b < NSB && good; b++) {
+      for (uint32_t b = 1; b < nact && good; b++) {
         const uint32_t xp = L.dexit[b - 1], cb = L.dcnt[b];
         uint32_t j = 0;
         if (cb != NONE32)
@@ -858,7 +863,7 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
         if (cb == NONE32 || j >= cb || L.fl[b * SECT + j].start != xp) {
           uint32_t x = xp, n = 0, lx = 0, lps = 0, lkey = 0, lkw = 0;
           const uint32_t end = (b + 1) * SB;
-          while (x < end && x < STOP) {
+          while (x < end && x < dstop) {
             uint32_t hl, plen, key, b01;
             if (n >= SECT || !parse_rel<G>(L, x, hl, plen, key, b01)) { good = false; break; }
             const uint32_t ps = x + hl, kw = rotr8(key, 0u - ps);
@@ -869,7 +874,7 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
             lx = x; lps = ps; lkey = key; lkw = kw;
             x = ps + plen;
           }
-          if (x < end && b + 1 < NSB) good = false;
+          if (x < end && b + 1 < nact) good = false;
           L.dcnt[b] = n;
           L.dexit[b] = x;
           if (n) L.dlast[b] = uint4{lx, lps, lkey, lkw};
@@ -916,10 +921,10 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
       e.kw = S0.cov_kw;
       L.fl[0] = e;
     }
-    uint32_t last = NSB - 1;  // the last sub-block with frames
+    uint32_t last = nact - 1;  // the last sub-block with frames
     while (last > 0 && L.dcnt[last] == L.dent[last]) last--;
     const uint4 f = L.dlast[last];
-    const uint32_t xe = L.dexit[NSB - 1];
+    const uint32_t xe = L.dexit[nact - 1];
     if (frames) {
       cstate S;
       S.cov_start = ss + f.x; S.cov_ps = ss + f.y; S.X = ss + xe;
@@ -1187,9 +1192,14 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
         const cstate S0 = L.S;
         const bool kn = L.known != 0, pst = L.past != 0;
         const uint64_t se14 = ss + G::SEG + XYWS_MAX_FRAME_HEADER_SIZE;
+        constexpr uint32_t STOP = G::SEG - XYWS_MAX_FRAME_HEADER_SIZE + 1;
+        // the successor's entry in this segment: the pass stops there (the
+        // serial chase below crosses it), beyond its first two sub-blocks
+        const bool hin = kn && !pst && L.hn < se14;
+        const uint32_t dstop = hin ? (L.hn - ss < STOP ? (uint32_t)(L.hn - ss) : STOP) : STOP;
         if (!(S0.st & (S_PARTIAL | S_CUT)) && S0.X >= ss && S0.X < ss + G::SB && P.hi >= se14 &&
-            (!kn || (L.Wn >= se14 && (pst || L.hn >= se14))))
-          dense = dense_pass<G>(P, L, ss, tid, (P.opts & XYWS_OPT_UNMASKED_HINT) != 0, pst);
+            (!kn || (hin ? (L.hn >= ss + 2 * G::SB && L.Wn >= L.hn) : L.Wn >= se14)))
+          dense = dense_pass<G>(P, L, ss, tid, (P.opts & XYWS_OPT_UNMASKED_HINT) != 0, pst, dstop);
       }
       if (tid < 64) {
         // lane 0 chases; then wave 0 classifies the rows (the other waves wait
