@@ -554,32 +554,23 @@ XYWS_DEV u32x4 chunk_xor(const lds_t<G>& L, uint32_t nfl, uint32_t g, uint32_t a
 // False for a payload length of 2^31 or more (left to the 64-bit parse).
 template <class G>
 XYWS_DEV bool parse_rel(const lds_t<G>& L, uint32_t x, uint32_t& hl, uint32_t& plen, uint32_t& key, uint32_t& b01) {
+  // (no branches: the three length forms and key positions are selected, so
+  // a chase step is one straight run of instructions after its LDS reads)
   const uint32_t* q = reinterpret_cast<const uint32_t*>(L.seg + (x & ~3u));
   const uint32_t sh = x & 3u, r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
   const uint32_t w0 = __builtin_amdgcn_alignbyte(r1, r0, sh), w1 = __builtin_amdgcn_alignbyte(r2, r1, sh);
+  const uint32_t w2 = __builtin_amdgcn_alignbyte(r3, r2, sh), w3 = __builtin_amdgcn_alignbyte(r4, r3, sh);
   b01 = w0 & 0xFFFFu;
-  const uint32_t b1 = (w0 >> 8) & 0xFFu, l7 = b1 & 0x7Fu, msk = b1 >> 7;
-  uint32_t ext;
-  if (l7 < 126) {
-    plen = l7; ext = 0;
-  } else if (l7 == 126) {
-    plen = ((w0 >> 8) & 0xFF00u) | (w0 >> 24); ext = 2;
-  } else {
-    const uint32_t w2 = __builtin_amdgcn_alignbyte(r3, r2, sh);
-    const uint32_t hi32 = __builtin_amdgcn_alignbyte(w1, w0, 2);  // bytes 2..5
-    const uint32_t lo32 = __builtin_amdgcn_alignbyte(w2, w1, 2);  // bytes 6..9
-    if (hi32 != 0u || (lo32 & 0x80u)) return false;
-    plen = __builtin_bswap32(lo32); ext = 8;
-  }
-  hl = 2 + ext + 4 * msk;
-  key = 0;
-  if (msk) {
-    if (ext == 0) key = __builtin_amdgcn_alignbyte(w1, w0, 2);
-    else if (ext == 2) key = w1;
-    else key = __builtin_amdgcn_alignbyte(__builtin_amdgcn_alignbyte(r4, r3, sh),
-                                          __builtin_amdgcn_alignbyte(r3, r2, sh), 2);
-  }
-  return true;
+  const uint32_t l7 = (w0 >> 8) & 0x7Fu, msk = (w0 >> 15) & 1u;
+  const bool s7 = l7 < 126, s16 = l7 == 126;
+  const uint32_t hi32 = __builtin_amdgcn_alignbyte(w1, w0, 2);  // bytes 2..5
+  const uint32_t lo32 = __builtin_amdgcn_alignbyte(w2, w1, 2);  // bytes 6..9
+  const uint32_t p16 = ((w0 >> 8) & 0xFF00u) | (w0 >> 24);
+  plen = s7 ? l7 : (s16 ? p16 : __builtin_bswap32(lo32));
+  hl = 2u + (s7 ? 0u : (s16 ? 2u : 8u)) + 4u * msk;
+  const uint32_t k = s7 ? hi32 : (s16 ? w1 : __builtin_amdgcn_alignbyte(w3, w2, 2));
+  key = msk ? k : 0u;
+  return s7 || s16 || (hi32 == 0u && !(lo32 & 0x80u));  // lengths >= 2^31: the general step
 }
 
 // Descriptors requested (lane 0): the k frames starting at frame-list entry
