@@ -453,7 +453,9 @@ def main():
                  "cyc_fill", "cyc_chase_sync", "cyc_xor", "cyc_tail", "cyc_prefetch_issue", "cyc_chase_pass",
                  "cyc_pro_fill", "cyc_pro_scan", "cyc_pro_publish", "dense_no_entry", "dense_chase_fail",
                  "dense_mismatch", "dense_overflow", "giveups", "bridges", "steal_requests", "steals",
-                 "stolen_segments", "cyc_dense_validate", "cyc_rows", "cyc_serial_chase"]
+                 "stolen_segments", "cyc_dense_validate", "cyc_rows", "cyc_serial_chase",
+                 "sweep_rechased", "sweep_pred_fail", "cyc_sweep_lookback", "cyc_sweep_scan", "cyc_sweep_spec",
+                 "sweep_slow_path", "sweep_scanned", "cyc_sweep_undecided"]
         for _ in range(2):
             dec.opts |= _lib.OPT_STATS
             dec.decode(bufs[0], cap=0, count=False, carry=False)

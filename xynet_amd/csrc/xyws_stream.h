@@ -13,6 +13,9 @@ struct stream_scratch {
   int ncu;              // compute units of the context's device (runs per launch)
   void* fmem;           // frame-start lists for descriptor emission (grown with the caller's cap)
   uint64_t fbytes;
+  void* smem;           // sweep decoder: per-segment granules, records and flag bitmap
+  uint64_t sbytes;
+  uint64_t max_segs;    // segments smem covers
 };
 
 void stream_scratch_init(stream_scratch* s, int device);
@@ -38,6 +41,14 @@ int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_ru
                                        // of a successor whose workgroup has not started; finish bridges it)
 #define XYWS_OPT_STEAL 0x400000u       // work stealing between runs (off by default: measured no faster on c1-c4)
 #define XYWS_OPT_TEST_STEAL 0x800000u  // tests: stealing on, every fourth run starts late, pieces of 1 segment and up
+#define XYWS_OPT_SWEEP 0x1000000u      // the sweep decoder (segment claiming) instead of the run decoder;
+                                       // calls without descriptors only (measured slower on c1-c4, opt-in)
+#define XYWS_OPT_SW_LATEPF 0x4000000u  // experiment (sweep): the next segment's loads issued after the entry scan
+#define XYWS_OPT_SW_FULLSCAN 0x8000000u  // experiment (sweep): scan the whole segment for an entry, not its first window
+#define XYWS_OPT_SWX_NOVAL 0x10000000u  // timing experiments only (wrong results possible): no deferred checks
+#define XYWS_OPT_SWX_NOREC 0x20000000u  // timing experiments only: no segment records
+#define XYWS_OPT_TEST_SPEC 0x2000000u  // tests (sweep decoder): segments 1, 4, 7, ... report no entry, segments
+                                       // 2, 5, 8, ... speculate one byte late (look-back fix-ups, repair walk)
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
                         const xyws_carry* cin, xyws_carry* cout, xyws_frame* frames, uint64_t cap,
                         uint64_t* nframes, uint32_t opts, hipStream_t stream);
