@@ -27,6 +27,7 @@ import ctypes as C
 import json
 import os
 import sys
+import statistics
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -169,19 +170,29 @@ def cpu_baseline(torch, buf, info, budget_s=12.0):
     host = buf[:sample_bytes].cpu().numpy().copy()
     threads = cpu_threads()
 
-    def rate(fn, nbytes_payload, budget):
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            fn()
-            reps += 1
-            dt = time.perf_counter() - t0
-            if dt >= budget:
-                return round(reps * nbytes_payload / dt / GIB, 4)
+    def rate(fn, nbytes_payload, budget, samples=5):
+        # the median of `samples` timed samples, each at least
+        # one whole pass over the sample and about budget / samples long
+        rates = []
+        for _ in range(samples):
+            reps, t0 = 0, time.perf_counter()
+            while True:
+                fn()
+                reps += 1
+                dt = time.perf_counter() - t0
+                if dt >= budget / samples:
+                    break
+            rates.append(reps * nbytes_payload / dt / GIB)
+        return round(statistics.median(rates), 4)
 
     small = host[: max(frame_bytes, min(host.size, 32 << 20) // max(frame_bytes, 1) * frame_bytes)].copy()
     pay_small = int(payload_sample * small.size / max(host.size, 1))
     O2 = Oracle()
     res = {"kind": "port", "unit": "GiB/s", "cores": threads, "nproc": os.cpu_count(),
+           "cores_reason": "the CPUs this process may run on (sched_getaffinity), capped by OMP_NUM_THREADS "
+                           f"({os.environ.get('OMP_NUM_THREADS', 'unset')}: the GPU box's CPU share; nproc shows "
+                           "the whole machine)",
+           "statistic": "median of 5 timed samples per figure",
            "sample": f"first {sample_bytes} B of this rank's batch (host copy, whole frames): "
                      f"oracle/xyws_oracle.c restatement -O2, serial header walk + unmask on {threads} threads",
            "value": rate(lambda: O2.decode_batch_mt(host, threads), payload_sample, budget_s * 0.4),
@@ -191,11 +202,16 @@ def cpu_baseline(torch, buf, info, budget_s=12.0):
         res["value_O0_1core"] = rate(lambda: O0.decode_batch_mt(small, 1), pay_small, budget_s * 0.1)
     except Exception:
         pass
-    if os.path.exists(ref_lib_path("O2")):  # the reference headers themselves (container-built)
+    sha_file = os.path.join(os.path.dirname(ref_lib_path("O2")), "SOURCE_SHA")
+    if os.path.exists(ref_lib_path("O2")) and not os.path.exists(sha_file):
+        res["reference"] = {"dropped": "oracle/_ref has no SOURCE_SHA stamp (not built by oracle/Makefile)"}
+    elif os.path.exists(ref_lib_path("O2")):  # the reference headers themselves (container-built)
         try:
             R = Reference("O2")
             ref = {"value": rate(lambda: R.decode_batch_mt(host, threads), payload_sample, budget_s * 0.2),
-                   "cores": threads}
+                   "cores": threads, "src_sha": open(sha_file).read().strip(),
+                   "src_sha_of": "oracle/Makefile: websocket_frame_header.h, websocket_frame_mask.h, "
+                                 "ref_harness.cpp, include/xyws.h"}
             if os.path.exists(ref_lib_path("O0")):
                 R0 = Reference("O0")
                 ref["value_O0_1core"] = rate(lambda: R0.decode_batch_mt(small, 1), pay_small, budget_s * 0.1)
@@ -297,6 +313,46 @@ def arena_path_rate(torch, ws, T, info, buf, golden, conns=4, recv=16 << 20):
             "device_error": err}
 
 
+def copy_ceiling(torch, ws, buf, reps=10):
+    """The same-box ceiling for this batch's traffic, measured in the run:
+    (a) an in-place XOR of the whole batch with one key (xyws_unmask,
+    k_unmask_range: every byte read and written once, no boundaries: the
+    decode's traffic with nothing to resolve), (b) a D2D hipMemcpy of the batch
+    into a scratch buffer (torch copy_). GB/s over `reps` launches each, HIP
+    events; an even number of XOR passes leaves the batch as it was."""
+    reps += reps % 2
+    stream = torch.cuda.current_stream()
+    ctx = ws.Context(buf.device.index or 0)
+    key = (C.c_uint8 * 4)(0x5A, 0xC3, 0x96, 0x21)
+    n = buf.numel()
+
+    def xor_pass():
+        assert ctx.L.xyws_unmask(ctx.h, C.c_void_p(buf.data_ptr()), n, key, 0, None,
+                                 C.c_void_p(stream.cuda_stream)) == 0
+
+    def timed(fn):
+        fn()
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    ms_xor = timed(xor_pass)
+    dst = torch.empty_like(buf)
+    ms_cpy = timed(lambda: dst.copy_(buf))
+    del dst
+    return {"unmask_inplace_gbs": round(2 * n / (ms_xor * 1e-3) / 1e9, 1),
+            "d2d_copy_gbs": round(2 * n / (ms_cpy * 1e-3) / 1e9, 1),
+            "bytes_per_launch": 2 * n, "reps": reps,
+            "what": "in-place XOR of the batch with one key (xyws_unmask) and D2D hipMemcpy of the batch, "
+                    "same device, in this run: read + write bytes / HIP-event time"}
+
+
 def source_hash():
     """Hash of the decoder sources, stamped on PMC records (profiles/pmc_traffic.json)
     so that a traffic figure is only reported for the kernel it was measured on."""
@@ -362,6 +418,7 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="fused", choices=["fused", "serial"])
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-ceiling", action="store_true", help="skip the in-run copy-ceiling measurement")
     ap.add_argument("--host-path", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--copies", type=int, default=0,
@@ -506,6 +563,11 @@ def main():
             host_rate["arena"] = arena_path_rate(torch, ws, T, info, bufs[0], golden)
 
     traffic, traffic_src = pmc_traffic(args.config, args.mode + ("+frames" if args.frames else ""))
+    ceiling = None
+    if rank == 0 and not args.no_ceiling:
+        ceiling = copy_ceiling(torch, ws, bufs[0])
+        ceiling["frac_vs_unmask"] = round(achieved / ceiling["unmask_inplace_gbs"], 4)
+        ceiling["frac_vs_d2d_copy"] = round(achieved / ceiling["d2d_copy_gbs"], 4)
 
     if rank == 0:
         line = {
@@ -545,6 +607,7 @@ def main():
                 "kernel_ms_note": "HIP-event time per decode over the timed steps (runs + finish kernels "
                                   "and the gaps between steps); per-kernel split: profiles/*_kernel_stats.csv",
                 "src_sha": source_hash(),
+                "copy_ceiling": ceiling,
             },
             "cpu_baseline": cpu,
             "parity": bool(parity_all) if parity_all is not None else None,

@@ -160,6 +160,16 @@ int xyws_ctx_last_device_error(xyws_ctx* ctx, uint32_t* out);
 int xyws_unmask(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4],
                 uint64_t phase, uint64_t* phase_out, void* stream);
 
+/* websocket_mask(R&& data, uint32_t mask, size_t i) with the reference's
+ * contract (websocket_frame_mask.h:14, called by websocket_recv_data at
+ * example/include/common/websocket.h:131): `data` is host or device memory,
+ * and the bytes are unmasked when the call returns (it synchronizes
+ * `stream`). Host bytes are staged through the context's device buffer (a
+ * compatibility path: two copies per call); device bytes go to xyws_unmask.
+ * Not allowed during stream capture (XYWS_ERR_CAPACITY). */
+int xyws_mask_bytes(xyws_ctx* ctx, void* data, uint64_t len, const uint8_t key[4],
+                    uint64_t phase, uint64_t* phase_out, void* stream);
+
 /* Frames at caller-known offsets (ascending, non-overlapping) inside one
  * device buffer: parse each header as websocket_frame_header_parser::parse
  * does from a fresh parser, then unmask its payload in place (clipped to the

@@ -8,8 +8,11 @@
 //     include/xynet/http/websocket_frame_header.h:42-106
 //   detail::calc_frame_header_size / calc_frame_size      xyws::detail::calc_frame_header_size
 //     :111-131, WS_MAX_FRAME_HEADER_SIZE :134               / calc_frame_size, WS_MAX_FRAME_HEADER_SIZE
-//   websocket_mask(R&& data, uint32_t mask, size_t i)     xyws::websocket_mask(ctx, dev span, mask, i)
-//     include/xynet/http/websocket_frame_mask.h:6-25        (device memory, in place, returns i+len)
+//   websocket_mask(R&& data, uint32_t mask, size_t i)     xyws::websocket_mask(data, mask, i): same
+//     include/xynet/http/websocket_frame_mask.h:6-25        signature (host or device bytes, done on
+//                                                           return); websocket_mask(ctx, dev span,
+//                                                           mask, i, stream): asynchronous, device
+//   using namespace xynet (websocket.h:17)                namespace xynet = the names below
 //   websocket_frame_header_parser::result()               xyws::frame::result()
 //     :264-267 -> tuple<flags, mask_uint32_t, length>
 //   websocket_recv_data: parse -> result -> mask          xyws::frame_decoder::decode
@@ -28,14 +31,17 @@
 #pragma once
 
 #include <array>
+#include <concepts>
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
+#include <ranges>
 #include <span>
 #include <string_view>
 #include <stdexcept>
 #include <string>
 #include <tuple>
+#include <type_traits>
 #include <utility>
 
 #include "../xyws.h"
@@ -147,6 +153,36 @@ inline std::size_t websocket_mask(context& ctx, std::span<std::byte> dev_data, s
   return static_cast<std::size_t>(out);
 }
 
+// The calling thread's context on device 0 (what default-constructed parsers
+// and the reference-signature websocket_mask use, so `websocket_frame_header_parser{}`
+// and `websocket_mask(data_span, mask, 0)` read as in the reference).
+inline context& default_context() {
+  thread_local context ctx(0);
+  return ctx;
+}
+
+// websocket_mask(R&& data, uint32_t mask, size_t i) with the reference's
+// signature and contract (websocket_frame_mask.h:6-25): any contiguous range
+// of byte-sized elements, host or device memory, unmasked in place when it
+// returns; returns i + size. On the device through xyws_mask_bytes (host
+// bytes staged: a compatibility path; batches go through frame_decoder).
+template <typename R>
+  requires std::ranges::contiguous_range<R> && std::ranges::sized_range<R> &&
+           (sizeof(std::ranges::range_value_t<R>) == 1) &&
+           (std::is_convertible_v<std::ranges::range_value_t<R>, std::byte> ||
+            std::is_convertible_v<std::ranges::range_value_t<R>, char> ||
+            std::is_convertible_v<std::ranges::range_value_t<R>, unsigned char> ||
+            std::is_same_v<std::ranges::range_value_t<R>, std::byte>)
+std::size_t websocket_mask(R&& data, std::uint32_t mask, std::size_t i) {
+  const std::uint8_t key[4] = {std::uint8_t(mask), std::uint8_t(mask >> 8), std::uint8_t(mask >> 16),
+                               std::uint8_t(mask >> 24)};
+  std::uint64_t out = 0;
+  check(xyws_mask_bytes(default_context().native(), const_cast<void*>(static_cast<const void*>(std::ranges::data(data))),
+                        std::ranges::size(data), key, i, &out, nullptr),
+        "xyws_mask_bytes");
+  return static_cast<std::size_t>(out);
+}
+
 // A decoded frame (device descriptor copied to the host by the caller).
 struct frame : xyws_frame {
   websocket_flags flags_() const noexcept { return websocket_flags(xyws_frame::flags); }
@@ -194,13 +230,6 @@ class frame_decoder {
   xyws_carry* carry_;
   std::uint32_t opts_;
 };
-
-// The calling thread's context on device 0 (what default-constructed parsers
-// use, so `websocket_frame_header_parser{}` reads as in the reference).
-inline context& default_context() {
-  thread_local context ctx(0);
-  return ctx;
-}
 
 // class websocket_frame_header (websocket_frame_header.h:179-224): a header in
 // a 14-byte array. As in the reference, the masked constructors keep the key
@@ -331,3 +360,10 @@ inline void classify_frames(context& ctx, std::span<const std::byte> dev_src, st
 }
 
 }  // namespace xyws
+
+// The reference's namespace (websocket_frame_header.h, `using namespace xynet`
+// at example/include/common/websocket.h:17): its frame names resolve to the
+// ones above, so a caller switches by include.
+namespace xynet {
+using namespace ::xyws;
+}

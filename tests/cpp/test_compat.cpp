@@ -1,0 +1,142 @@
+// A websocket.h-shaped caller switched to the shim by include alone.
+//
+// websocket_recv_data (example/include/common/websocket.h:110-134) is kept in
+// shape: `using namespace xynet; using namespace std;` (:17-18), a default-
+// constructed websocket_frame_header_parser, parse() on the growing prefix of
+// a host receive buffer, result() as a structured binding, and
+// websocket_mask(data_span, mask, 0) with the reference's three-argument
+// signature (websocket_frame_mask.h:14). Only its two frame includes (:10-11)
+// became the shim's; the socket is a stand-in whose recv_some hands out the
+// next piece of a prepared wire (no coroutines: co_await dropped).
+// Frames arrive in pieces of 14-1024 B after a first piece holding the header.
+//
+// Prints "ok N" after N frames received and checked.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "xyws/websocket.hpp"  // was xynet/http/websocket_frame_header.h + websocket_frame_mask.h
+
+inline constexpr static const uint16_t MAX_HTTP_REQUEST_SIZE = 1024;
+
+using namespace xynet;
+using namespace std;
+
+struct stand_in_socket {
+  vector<byte> wire;
+  size_t pos = 0, piece = 1;
+  size_t recv_some(span<byte> dst) {
+    size_t n = min({piece, dst.size(), wire.size() - pos});
+    memcpy(dst.data(), wire.data() + pos, n);
+    pos += n;
+    return n;
+  }
+};
+
+auto websocket_recv_data(stand_in_socket& peer_socket, auto& buf) -> decltype(std::span{buf.data(), 0u}) {
+  auto recv_bytes = size_t{};
+  auto parser = websocket_frame_header_parser{};
+
+  while (recv_bytes < MAX_HTTP_REQUEST_SIZE) {
+    recv_bytes += peer_socket.recv_some(std::span{buf.data() + recv_bytes, buf.size() - recv_bytes});
+
+    if (auto ret = parser.parse(std::span{buf.data(), recv_bytes}); ret == UINT32_MAX) {
+      continue;
+    } else if (ret == websocket_frame_header_parser::npos) {
+      continue;  // (the reference compares with UINT32_MAX, never npos: its loop
+                 // would go on with ret = npos; the stand-in keeps receiving)
+    } else {
+      auto [flags, mask, length] = parser.result();
+      if (!websocket_flags_not_none(flags & websocket_flags::WS_HAS_MASK)) return {};
+      while (recv_bytes < ret + length)  // (the reference's caller receives the rest elsewhere)
+        recv_bytes += peer_socket.recv_some(std::span{buf.data() + recv_bytes, buf.size() - recv_bytes});
+      auto data_span = std::span{buf.data() + ret, length};
+      websocket_mask(data_span, mask, 0);
+      return data_span;
+    }
+  }
+  return {};
+}
+
+// --latency: the per-header cost of the compatibility path (one device round
+// trip per parse() and per websocket_mask call), averaged over 2000 frames of
+// 125 B received whole.
+static int latency() {
+  const uint32_t key = 0x9a8b7c6du;
+  const auto h = websocket_frame_header::with_key(websocket_flags::WS_OP_BINARY | websocket_flags::WS_FINAL_FRAME, key, 125);
+  stand_in_socket sock;
+  sock.piece = 1024;
+  array<byte, MAX_HTTP_REQUEST_SIZE + 64> buf{};
+  const int n = 2000;
+  double t_parse = 0, t_mask = 0;
+  for (int it = 0; it < n + 50; it++) {
+    sock.wire.assign(h.span().begin(), h.span().end());
+    sock.wire.resize(h.span().size() + 125, byte{0});
+    sock.pos = 0;
+    size_t got = sock.recv_some(std::span{buf.data(), buf.size()});
+    auto parser = websocket_frame_header_parser{};
+    const auto t0 = chrono::steady_clock::now();
+    const size_t ret = parser.parse(std::span{buf.data(), got});
+    const auto t1 = chrono::steady_clock::now();
+    auto [flags, mask, length] = parser.result();
+    (void)flags;
+    auto data_span = std::span{buf.data() + ret, length};
+    websocket_mask(data_span, mask, 0);
+    const auto t2 = chrono::steady_clock::now();
+    if (it >= 50) {
+      t_parse += chrono::duration<double, micro>(t1 - t0).count();
+      t_mask += chrono::duration<double, micro>(t2 - t1).count();
+    }
+  }
+  printf("{\"parse_us\": %.2f, \"mask_host_125B_us\": %.2f, \"frames\": %d}\n", t_parse / n, t_mask / n, n);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "--latency")) return latency();
+  int ok = 0;
+  const size_t lens[] = {0, 1, 5, 125, 126, 127, 300, 1000};
+  // (the caller re-feeds the whole prefix to an incremental parser, as the
+  // reference's does: it is right when the first recv holds the whole header,
+  // which every piece size here guarantees; split headers are the golden split
+  // tests' subject, tests/cpp/test_shim.cpp)
+  const size_t pieces[] = {14, 20, 333, 1024};
+  uint32_t seed = 12345;
+  for (size_t len : lens) {
+    for (size_t piece : pieces) {
+      vector<byte> payload(len);
+      for (auto& b : payload) {
+        seed = seed * 1103515245u + 12345u;
+        b = byte((seed >> 16) & 0xFF);
+      }
+      const uint32_t key = seed * 2654435761u;
+      const auto h = websocket_frame_header::with_key(websocket_flags::WS_OP_TEXT | websocket_flags::WS_FINAL_FRAME,
+                                                      key, len);
+      stand_in_socket sock;
+      sock.piece = piece;
+      sock.wire.assign(h.span().begin(), h.span().end());
+      const auto* kb = reinterpret_cast<const unsigned char*>(&key);
+      for (size_t j = 0; j < len; j++) sock.wire.push_back(payload[j] ^ byte(kb[j % 4]));
+      array<byte, MAX_HTTP_REQUEST_SIZE + 64> buf{};
+      auto got = websocket_recv_data(sock, buf);
+      if (got.size() != len || (len && memcmp(got.data(), payload.data(), len) != 0)) {
+        printf("FAIL len %zu piece %zu: got %zu bytes\n", len, piece, got.size());
+        return 1;
+      }
+      ok++;
+    }
+  }
+  // the three-argument form on a phase other than 0, and its return value
+  {
+    vector<unsigned char> v(37, 0);
+    const uint32_t key = 0x44332211u;
+    const size_t r = websocket_mask(v, key, 6);
+    for (size_t j = 0; j < v.size(); j++)
+      if (v[j] != (unsigned char)(key >> (8 * ((6 + j) % 4)))) { printf("FAIL phase byte %zu\n", j); return 1; }
+    if (r != 43) { printf("FAIL return %zu\n", r); return 1; }
+    ok++;
+  }
+  printf("ok %d\n", ok);
+  return 0;
+}

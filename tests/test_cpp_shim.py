@@ -93,3 +93,27 @@ def test_cpp_shim_program_on_device(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     n = 9 + len(load_golden("frame_header.json")["splits"]) + len(load_golden("frame_header.json")["builds"])
     assert f"ok {n}" in r.stdout, r.stdout
+
+
+COMPAT_SRC = os.path.join(ROOT, "tests", "cpp", "test_compat.cpp")
+COMPAT_BIN = os.path.join(ROOT, "tests", "cpp", "test_compat")
+
+
+def test_websocket_h_caller_switches_by_include():
+    """websocket_recv_data in shape (websocket.h:110-134: `using namespace
+    xynet`, websocket_frame_header_parser{}, the three-argument
+    websocket_mask of websocket_frame_mask.h:14) compiles against the shim."""
+    r = subprocess.run(["g++", "-std=c++20", "-Wall", "-Werror", "-fsyntax-only", "-I", os.path.join(ROOT, "include"),
+                        COMPAT_SRC], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.gpu
+def test_websocket_h_caller_on_device():
+    """The same program run: 32 frames (0-1000 B payloads, received in pieces
+    of 14-1024 B) parsed and unmasked from host buffers, plus the
+    three-argument mask at phase 6 (its return i + len)."""
+    assert os.path.exists(COMPAT_BIN), "tests/cpp/test_compat not built (run __graft_entry__.build())"
+    r = subprocess.run([COMPAT_BIN], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok 33" in r.stdout, r.stdout

@@ -129,6 +129,8 @@ def load():
     L.xyws_ctx_last_device_error.argtypes = [vp, C.POINTER(u32)]
     L.xyws_unmask.restype = i32
     L.xyws_unmask.argtypes = [vp, vp, u64, vp, u64, C.POINTER(u64), vp]
+    L.xyws_mask_bytes.restype = i32
+    L.xyws_mask_bytes.argtypes = [vp, vp, u64, vp, u64, C.POINTER(u64), vp]
     L.xyws_decode_indexed.restype = i32
     L.xyws_decode_indexed.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp]
     L.xyws_debug_stats.restype = i32

@@ -57,7 +57,7 @@ def build(force=False, verbose=False, extra=None):
 # C++ callers of the header-only shim (include/xyws/websocket.hpp), run by the
 # GPU tests: linked against the in-tree libxyws.so (rpath), built here so the
 # binary travels to the GPU box with the tree.
-CPP_TESTS = {"tests/cpp/test_shim": "tests/cpp/test_shim.cpp"}
+CPP_TESTS = {"tests/cpp/test_shim": "tests/cpp/test_shim.cpp", "tests/cpp/test_compat": "tests/cpp/test_compat.cpp"}
 
 
 def build_cpp_tests(hipcc, force=False, verbose=False):

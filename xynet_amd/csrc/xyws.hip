@@ -295,6 +295,8 @@ int xyws_ctx_create(int device, xyws_ctx** out) {
   c->err = nullptr;
   c->reserve_bytes = 0;
   c->reserve_frames = 0;
+  c->stage = nullptr;
+  c->stage_cap = 0;
   for (auto& sl : c->slot) {
     sl.bound = false;
     sl.stream = nullptr;
@@ -328,6 +330,7 @@ int xyws_ctx_destroy(xyws_ctx* ctx) {
       stream_scratch_free(&sl.ss);
     }
     if (ctx->err) (void)hipFree(ctx->err);
+    if (ctx->stage) (void)hipFree(ctx->stage);
   }
   delete ctx;
   return XYWS_OK;
@@ -411,6 +414,45 @@ int xyws_unmask(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4], ui
   hipLaunchKernelGGL(k_unmask_range, dim3(grid_for(chunks, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, base, lo, hi, kw);
   return hip_err(hipGetLastError());
+}
+
+// websocket_mask with the reference's contract (websocket_frame_mask.h:14,
+// called at example/include/common/websocket.h:131): host or device bytes,
+// done when it returns. Device bytes are unmasked in place; host bytes go
+// through the context's device stage (copy in, k_unmask_range, copy out).
+int xyws_mask_bytes(xyws_ctx* ctx, void* data, uint64_t len, const uint8_t key[4], uint64_t phase,
+                    uint64_t* phase_out, void* stream) {
+  if (!ctx || !key || (!data && len)) return XYWS_ERR_INVALID;
+  if (phase_out) *phase_out = phase + len;
+  if (!len) return XYWS_OK;
+  device_guard g(ctx->device);
+  if (!g.ok) return XYWS_ERR_HIP;
+  hipStream_t s = (hipStream_t)stream;
+  if (capturing(s)) return XYWS_ERR_CAPACITY;  // (synchronous by contract)
+  hipPointerAttribute_t attr;
+  const bool on_dev = hipPointerGetAttributes(&attr, data) == hipSuccess && attr.type == hipMemoryTypeDevice;
+  (void)hipGetLastError();  // (an unregistered host pointer leaves an error behind)
+  if (on_dev) {
+    if (const int rc = xyws_unmask(ctx, data, len, key, phase, nullptr, stream)) return rc;
+    return hip_err(hipStreamSynchronize(s));
+  }
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (ctx->stage_cap < len) {
+    if (ctx->stage) {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(ctx->stage);
+      ctx->stage = nullptr;
+      ctx->stage_cap = 0;
+    }
+    const uint64_t cap = len < 4096 ? 4096 : len;
+    if (hipMalloc(&ctx->stage, cap) != hipSuccess) return XYWS_ERR_NOMEM;
+    ctx->stage_cap = cap;
+  }
+  // the stage keeps the bytes' 16-byte phase, so the kernel sees the same lanes
+  if (hipMemcpyAsync(ctx->stage, data, len, hipMemcpyHostToDevice, s) != hipSuccess) return XYWS_ERR_HIP;
+  if (const int rc = xyws_unmask(ctx, ctx->stage, len, key, phase, nullptr, stream)) return rc;
+  if (hipMemcpyAsync(data, ctx->stage, len, hipMemcpyDeviceToHost, s) != hipSuccess) return XYWS_ERR_HIP;
+  return hip_err(hipStreamSynchronize(s));
 }
 
 int xyws_decode_indexed(xyws_ctx* ctx, void* dev_buf, uint64_t len, const uint64_t* dev_starts,

@@ -45,6 +45,8 @@ struct xyws_ctx {
   std::mutex mu;
   uint32_t* err;  // device error word (serial / indexed modes)
   uint64_t reserve_bytes, reserve_frames;  // applied to every slot
+  void* stage;          // xyws_mask_bytes: device copy of host bytes (under mu)
+  uint64_t stage_cap;
   scratch_slot slot[XYWS_SLOTS];
 };
 

@@ -47,6 +47,7 @@ int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_ru
 #define XYWS_OPT_SW_FULLSCAN 0x8000000u  // experiment (sweep): scan the whole segment for an entry, not its first window
 #define XYWS_OPT_SWX_NOVAL 0x10000000u  // timing experiments only (wrong results possible): no deferred checks
 #define XYWS_OPT_SWX_NOREC 0x20000000u  // timing experiments only: no segment records
+#define XYWS_OPT_SW_LOADWAIT 0x40000000u  // experiment (sweep): the next segment's loads land before the stores issue
 #define XYWS_OPT_TEST_SPEC 0x2000000u  // tests (sweep decoder): segments 1, 4, 7, ... report no entry, segments
                                        // 2, 5, 8, ... speculate one byte late (look-back fix-ups, repair walk)
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,

@@ -300,6 +300,7 @@ struct __attribute__((aligned(16))) lds_t {
   uint64_t sw_cur, sw_next, sw_ahead, sw_h, sw_ref, sw_fsz, sw_pcur, sw_fcur, sw_vs;
   cstate sw_spec, sw_in, sw_vU;
   uint32_t sw_act, sw_single, sw_cnt_spec, sw_fast, sw_padok;
+  uint64_t sw_t[9];  // sweep timing split (XYWS_OPT_STATS): see ST_SWT_*
 };
 
 // ---------------------------------------------------------------- small helpers
@@ -2505,6 +2506,14 @@ __global__ void k_stream_empty(const xyws_carry* cin, xyws_carry* cout, uint64_t
 enum { SR_U = 0, SR_F = 5, SR_H = 10, SR_CNT = 11, SR_WORDS = 12 };
 constexpr uint64_t XCLAMP = (1ull << 46) - 1;  // published positions (batches are below 2^46 bytes)
 constexpr uint32_t SPIN_SW = 1u << 20;          // bounded look-back polls (~1 s)
+// sweep timing split (shader clocks, summed over workgroups): tid 0 (the
+// control wave) waiting for its claim at the fill, its phase A, its phase B;
+// tid 64 (a data wave) from its loads' issue to the phase barrier, waiting for
+// its loads, issuing its stores, from the loop top to its fill's end, and the
+// whole iteration (ST_T_XOR stays the record/epilogue time)
+enum { ST_SWT_CLAIMW = 16, ST_SWT_A, ST_SWT_B, ST_SWT_DBAR, ST_SWT_DLOAD, ST_SWT_DSTORE = 22, ST_SWT_DFILL,
+       ST_SWT_ITER, ST_SWT_PRED };  // (PRED: phase A up to the entering state)
+XYWS_DEV uint64_t swt_now(const run_params& P) { return stats_on(P) ? __builtin_amdgcn_s_memtime() : 0; }
 enum { ST_SW_APPLY = 40, ST_SW_NOTHING, ST_SW_TLB, ST_SW_TSCAN, ST_SW_TSPEC, ST_SW_DEFER, ST_SW_WIN, ST_SW_TUND };
 // sweep actions
 enum { SW_REUSE = 0, SW_APPLY = 1, SW_NOTHING = 2 };
@@ -2820,35 +2829,43 @@ struct sweep_io {
   u32x4 e[K];
   XYWS_DEV static bool data_wave(uint32_t wave) { return !CTRL || wave != 0; }
   XYWS_DEV static uint32_t row(uint32_t wave, uint32_t k) { return (CTRL ? wave - 1 : wave) + NDW * k; }
-  // this wave's rows of the segment at ss into registers
+  // (a wave's row index is wave-uniform: a scalar offset, or hipcc loops over
+  // the lanes' values; rows past the segment load and store nothing)
+  XYWS_DEV static bool valid(uint32_t wave, uint32_t k) { return K * NDW == NROW || row(wave, k) < NROW; }
+  // this wave's rows of the segment at ss into registers: K loads on every
+  // path (the fill's wait then counts them)
+  // (CHK false: the caller is a data wave, so every path issues the same
+  // operations and the compiler's waits count them)
+  template <bool CHK = true>
   XYWS_DEV void issue(const run_params& P, uint64_t ss, uint32_t tid) {
-    const uint32_t wave = tid >> 6, lane = tid & 63u;
-    if (!data_wave(wave)) return;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
+    if (CHK && !data_wave(wave)) return;
     const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss);
 #pragma unroll
     for (uint32_t k = 0; k < K; k++) {
       const uint32_t r = row(wave, k);
-      if (K * NDW == NROW || r < NROW) e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16u, r * 1024u, AUX_NT);
+      e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, valid(wave, k) ? lane * 16u : OOB, r * 1024u, AUX_NT);
     }
   }
   // K dropped stores (the out-of-range offset: no memory traffic) after the
   // first loads, as the stores after every later segment's loads
+  template <bool CHK = true>
   XYWS_DEV static void dummy(const run_params& P, uint64_t ss, uint32_t tid) {
-    const uint32_t wave = tid >> 6, lane = tid & 63u;
-    if (!data_wave(wave)) return;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
+    if (CHK && !data_wave(wave)) return;
     const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss);
 #pragma unroll
     for (uint32_t k = 0; k < K; k++)
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rs, OOB, k * 1024u, AUX_ST);
   }
-  template <class LT>
+  template <bool CHK = true, class LT>
   XYWS_DEV void fill(LT& L, uint32_t tid) const {
-    const uint32_t wave = tid >> 6, lane = tid & 63u;
-    if (!data_wave(wave)) return;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
+    if (CHK && !data_wave(wave)) return;
 #pragma unroll
     for (uint32_t k = 0; k < K; k++) {
       const uint32_t r = row(wave, k);
-      if (K * NDW == NROW || r < NROW) *reinterpret_cast<u32x4*>(&L.seg[r * 1024u + lane * 16u]) = e[k];
+      if (valid(wave, k)) *reinterpret_cast<u32x4*>(&L.seg[r * 1024u + lane * 16u]) = e[k];
     }
   }
 };
@@ -2856,19 +2873,20 @@ struct sweep_io {
 // XOR stores of a segment's rows by the data waves (sweep_io's layout): one
 // 16-byte store per chunk (skipped ones to the out-of-range offset), then the
 // chunks holding a frame boundary or a write-window edge (store_pass).
-template <class G>
+template <class G, bool CHK = true>
 XYWS_DEV void store_rows(const run_params& P, const lds_t<G>& L, uint64_t ss, uint32_t tid, uint32_t nfl,
                          uint32_t hi_c, uint64_t wl, uint64_t whi, uint32_t wl_r, uint32_t wh_r) {
   using IO = sweep_io<G>;
-  const uint32_t wave = tid >> 6, lane = tid & 63u;
-  if (!IO::data_wave(wave)) return;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
+  if (CHK && !IO::data_wave(wave)) return;
   const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss);
   uint32_t edge = 0;
   u32x4 dprev = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (uint32_t k = 0; k < IO::K; k++) {
-    const uint32_t r = IO::row(wave, k);
-    if (!(IO::K * IO::NDW == IO::NROW || r < IO::NROW)) continue;
+    // (K stores on every path: a row past the segment stores nothing)
+    const bool ok = IO::valid(wave, k);
+    const uint32_t r = ok ? IO::row(wave, k) : 0u;
     const uint32_t a = r * 1024u + lane * 16u;
     const uint2 rw = L.rt[r];
     const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
@@ -2904,6 +2922,10 @@ XYWS_DEV void store_rows(const run_params& P, const lds_t<G>& L, uint64_t ss, ui
           edge |= 1u << k;
         }
       }
+    }
+    if (!ok) {
+      off = OOB;
+      edge &= ~(1u << k);
     }
     const u32x4 d = v ^ m;
     __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, r * 1024u, AUX_ST);
@@ -3222,9 +3244,16 @@ XYWS_DEV uint32_t sweep_slow(const run_params& P, lds_t<G>& L, uint32_t tid, uin
 //    none (EXACT: look back first, then chase).
 // Every segment publishes its exit; a segment whose final exit differs from
 // its publication counts in HW_BAD (the finisher's repair walk).
-template <class G>
+// ROLE: the waves running this copy. With a control wave (sweep_io::CTRL) the
+// kernel runs two loops, one per role, with the same barriers: the control
+// wave's state (64-bit chain states, look-back) and the data waves' prefetch
+// registers then never share a register allocation region (one loop holding
+// both spilled the prefetch and waited for every load at each store).
+enum { SWR_ALL = 0, SWR_CTRL = 1, SWR_DATA = 2 };
+template <class G, int ROLE>
 XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, uint64_t s, sweep_io<G>& io,
                                 uint32_t cr[5], uint32_t& claimed, uint64_t nx) {
+  constexpr bool CT = ROLE != SWR_DATA, DT = ROLE != SWR_CTRL;
   const uint64_t ss = s * G::SEG;
   const uint64_t E = L.E;
   const bool unm = (P.opts & XYWS_OPT_UNMASKED_HINT) != 0;
@@ -3237,7 +3266,7 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
   //    its publication (FAST). The dense pass, the quick scan, the SPEC and
   //    EXACT modes and several passes are the slow path below, after every
   //    wave's loads are out.
-  if (tid == 0) {
+  if (CT && tid == 0) {
     // this segment's first bytes for the segment before it (sweep_pad)
     sweep_orig_publish(P, s, E, *reinterpret_cast<const u32x4*>(L.seg));
     sweep_chain_reset(L);
@@ -3267,6 +3296,7 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
       }
     }
     L.sw_act = mode;
+    if (st_on) L.sw_t[8] += __builtin_amdgcn_s_memtime() - tq;
     uint32_t fast = 0;
     if ((mode == SWM_EXACT0 || mode == SWM_PRED) && !(L.sw_in.st & S_PARTIAL) && L.dense < 2 * G::NSB) {
       L.S = L.sw_in;
@@ -3287,12 +3317,13 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
       L.sw_pcur = pn;  // (consumed when the next segment starts: see the loop)
       L.sw_fcur = L.sw_fsz;
     }
+    if (st_on) L.sw_t[1] += __builtin_amdgcn_s_memtime() - tq;
   }
   // the next segment's loads (wave 0 after its work above; lane 0's claim and
   // header loads first, so that the data loads are the youngest and the fill
   // waits for them while this segment's stores still drain)
   if (nx < P.nseg) {
-    if (tid == 0) {
+    if (CT && tid == 0) {
       // the claim of the segment after the next one: a returning atomic whose
       // value is read only when the next segment's loads have been waited
       // for (inline asm: the compiler's atomic optimizer would wait for it,
@@ -3301,11 +3332,12 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
       const uint64_t pn = L.sw_pcur;
       if (pn != NONE && pn >= L.sw_fcur) cover_load(P, pn - L.sw_fcur, cr);
     }
-    io.issue(P, nx * G::SEG, tid);
+    if constexpr (DT) io.template issue<ROLE == SWR_ALL>(P, nx * G::SEG, tid);
   }
+  const uint64_t tb0 = swt_now(P);
   // B. fast: wave 0 builds the row table while the other waves' loads fly,
   //    then checks the previous predicted segment
-  if (tid < 64) {
+  if (CT && tid < 64) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -3321,8 +3353,10 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
       sweep_validate(P, vs, vs * G::SEG, E, tid, L.sw_vU);
       if (tid == 0) L.sw_vs = NONE;
     }
+    if (tid == 0 && stats_on(P)) L.sw_t[2] += __builtin_amdgcn_s_memtime() - tb0;
   }
   __syncthreads();
+  if (tid == 64 && stats_on(P)) L.sw_t[3] += __builtin_amdgcn_s_memtime() - tb0;
   if (st_on) {
     const uint64_t t = __builtin_amdgcn_s_memtime();
     stat_add(P, ST_SW_TSCAN, t - tq);
@@ -3344,7 +3378,7 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
     const uint64_t wl = P.lo, whi = P.hi;
     const uint32_t wl_r = wl > ss ? (wl - ss < G::SEG ? (uint32_t)(wl - ss) : G::SEG) : 0u;
     const uint32_t wh_r = whi > ss ? (whi - ss < G::SEG ? (uint32_t)(whi - ss) : G::SEG) : 0u;
-    if (tid < 64) {
+    if (CT && tid < 64) {
       if (act != SW_REUSE) {
         for (uint32_t r = tid; r < G::SEG / 1024; r += 64) L.rt[r] = uint2{ROW_SKIP, 0u};
       } else if (!fast) {
@@ -3352,13 +3386,21 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
         build_rows<G>(L, L.nfl, 0u, G::SEG, wl_r, wh_r, any, tid);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t tl0 = swt_now(P);
+    // (XYWS_OPT_SW_LOADWAIT, an experiment: the next segment's loads land
+    // before this segment's stores issue)
+    if (DT && (P.opts & XYWS_OPT_SW_LOADWAIT)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 64 && stats_on(P)) L.sw_t[4] += __builtin_amdgcn_s_memtime() - tl0;
     __syncthreads();
-    store_rows<G>(P, L, ss, tid, act == SW_REUSE ? L.nfl : 0u, act == SW_REUSE ? G::SEG : 0u, wl, whi, wl_r, wh_r);
+    const uint64_t ts0 = swt_now(P);
+    if constexpr (DT)
+      store_rows<G, ROLE == SWR_ALL>(P, L, ss, tid, act == SW_REUSE ? L.nfl : 0u, act == SW_REUSE ? G::SEG : 0u, wl,
+                                     whi, wl_r, wh_r);
+    if (tid == 64 && stats_on(P)) L.sw_t[5] += __builtin_amdgcn_s_memtime() - ts0;
   }
   __syncthreads();
   uint64_t cnt = 0;
-  if (tid == 0) {
+  if (CT && tid == 0) {
     cstate F;
     if (act == SW_REUSE) { F = L.sw_spec; cnt = L.sw_cnt_spec; }
     else if (act == SW_APPLY) { F = L.S; cnt = L.cnt; }
@@ -3508,6 +3550,55 @@ XYWS_DEV void sweep_finish(const run_params& P, lds_t<G>& L, uint32_t tid) {
   }
 }
 
+// The segment loop of one role (sweep_segment): the data waves prefetch the
+// next segment into registers and fill LDS from them; the control wave takes
+// the claims. Returns lane 0's frame count.
+template <class G, int ROLE>
+XYWS_DEV uint64_t sweep_loop(const run_params& P, lds_t<G>& L, uint32_t tid0, uint32_t& claimed) {
+  constexpr bool CT = ROLE != SWR_DATA, DT = ROLE != SWR_CTRL;
+  uint32_t tid = tid0;
+  asm volatile("" : "+v"(tid));
+  sweep_io<G> io;
+  uint32_t cr[5] = {0u, 0u, 0u, 0u, 0u};  // lane 0: its predicted predecessor header (sweep_predicted)
+  uint64_t frames = 0;                     // lane 0
+  uint64_t cur = uniform64(L.sw_cur);
+  if (DT && cur < P.nseg) {
+    io.template issue<ROLE == SWR_ALL>(P, cur * G::SEG, tid);
+    sweep_io<G>::template dummy<ROLE == SWR_ALL>(P, cur * G::SEG, tid);  // (as after every segment: stores younger than the loads)
+  }
+  while (cur < P.nseg) {
+    // (the lane index made opaque per segment: hipcc would otherwise hoist the
+    // lanes' address math out of this loop and spill it)
+    asm volatile("" : "+v"(tid));
+    const uint64_t ti0 = swt_now(P);
+    __syncthreads();  // the previous segment's LDS reads are done
+    if constexpr (DT) io.template fill<ROLE == SWR_ALL>(L, tid);
+    if (tid == 64 && stats_on(P)) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      L.sw_t[6] += __builtin_amdgcn_s_memtime() - ti0;
+    }
+    if (CT && tid == 0) {
+      const uint64_t tc0 = swt_now(P);
+      // the bytes after the segment: unknown (stale in LDS; the speculation
+      // may read them) until a header straddles its end (sweep_pad)
+      L.sw_padok = 0;
+      // the segment claimed during the previous segment (lane 0's atomic:
+      // wave 0 waits for its own few memory operations)
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(claimed)::"memory");
+      L.sw_next = claimed < P.nseg ? claimed : NONE;
+      if (stats_on(P)) L.sw_t[0] += __builtin_amdgcn_s_memtime() - tc0;
+    }
+    __syncthreads();
+    const uint64_t nx = uniform64(L.sw_next);
+    frames += sweep_segment<G, ROLE>(P, L, tid, cur, io, cr, claimed, nx);
+    if (tid == 64 && stats_on(P)) L.sw_t[7] += __builtin_amdgcn_s_memtime() - ti0;
+    cur = nx;
+  }
+  // the last predicted segment's check
+  if (CT && tid < 64 && L.sw_vs != NONE) sweep_validate(P, L.sw_vs, L.sw_vs * G::SEG, L.E, tid, L.sw_vU);
+  return frames;
+}
+
 template <class G>
 __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_sweep(run_params P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
@@ -3526,40 +3617,30 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_sweep(run_params P) {
     L.sw_pcur = NONE;
     L.sw_fcur = 0;
     L.sw_vs = NONE;
+#pragma unroll
+    for (int i = 0; i < 9; i++) L.sw_t[i] = 0;
   }
   __syncthreads();
-  uint32_t tid = tid0;
-  asm volatile("" : "+v"(tid));
-  sweep_io<G> io;
-  uint32_t cr[5] = {0u, 0u, 0u, 0u, 0u};  // lane 0: its predicted predecessor header (sweep_predicted)
-  uint64_t frames = 0;            // lane 0
-  uint64_t cur = uniform64(L.sw_cur);
-  if (cur < P.nseg) {
-    io.issue(P, cur * G::SEG, tid);
-    sweep_io<G>::dummy(P, cur * G::SEG, tid);  // (as after every segment: stores younger than the loads)
+  uint64_t frames = 0;  // lane 0
+  if constexpr (sweep_io<G>::CTRL) {
+    // (a wave-uniform branch the compiler sees as one: each loop is a scalar
+    // branch target, never an exec-masked region whose barriers another
+    // wave would not meet)
+    if (__builtin_amdgcn_readfirstlane(tid0 >> 6) == 0) frames = sweep_loop<G, SWR_CTRL>(P, L, tid0, claimed);
+    else (void)sweep_loop<G, SWR_DATA>(P, L, tid0, claimed);
+  } else {
+    frames = sweep_loop<G, SWR_ALL>(P, L, tid0, claimed);
   }
-  while (cur < P.nseg) {
-    // (the lane index made opaque per segment: hipcc would otherwise hoist the
-    // lanes' address math out of this loop and spill it)
-    asm volatile("" : "+v"(tid));
-    __syncthreads();  // the previous segment's LDS reads are done
-    io.fill(L, tid);
-    if (tid == 0) {
-      // the bytes after the segment: unknown (stale in LDS; the speculation
-      // may read them) until a header straddles its end (sweep_pad)
-      L.sw_padok = 0;
-      // the segment claimed during the previous segment (lane 0's atomic:
-      // wave 0 waits for its own few memory operations)
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(claimed)::"memory");
-      L.sw_next = claimed < P.nseg ? claimed : NONE;
-    }
+  if (stats_on(P)) {
     __syncthreads();
-    const uint64_t nx = uniform64(L.sw_next);
-    frames += sweep_segment<G>(P, L, tid, cur, io, cr, claimed, nx);
-    cur = nx;
+    if (tid0 == 0) {
+      const uint32_t slot[8] = {ST_SWT_CLAIMW, ST_SWT_A, ST_SWT_B, ST_SWT_DBAR, ST_SWT_DLOAD, ST_SWT_DSTORE,
+                                ST_SWT_DFILL, ST_SWT_ITER};
+#pragma unroll
+      for (int i = 0; i < 8; i++) stat_add(P, slot[i], L.sw_t[i]);
+      stat_add(P, ST_SWT_PRED, L.sw_t[8]);
+    }
   }
-  // the last predicted segment's check
-  if (tid < 64 && L.sw_vs != NONE) sweep_validate(P, L.sw_vs, L.sw_vs * G::SEG, L.E, tid, L.sw_vU);
   if (tid0 == 0 && frames)
     __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(P.head) + HW_TOTAL, frames, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
