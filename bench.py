@@ -381,6 +381,111 @@ def pmc_traffic(config, mode):
     return rec["hbm_bytes_per_launch"], f"profiles/pmc_traffic.json {config}:{mode} ({rec.get('profile', '?')})"
 
 
+# --op: the §8(f) callers on the decoded batch (tests/golden/gen_ops_golden.py
+# holds the same parameters and writes the expected digests)
+OP_PARAMS = {"enc_flags": 0x11, "cls_max_payload": 1 << 20, "cls_policy": 0x1, "rs_opts": 0x1}
+OP_GOLDEN_KEYS = {"c1": "c1_text_4k", "c2": "c2_bin_256", "c3": "c3_bin_64k", "c4": "c4_mixed"}
+
+
+def op_bench(args, torch, T, ws, info, buf):
+    """One §8(f) caller timed over the decoded batch (not the headline):
+    encode = echo_once's replies for every frame (xyws_encode_frames),
+    classify = the close policy per frame (xyws_classify_frames), reassemble =
+    FIN=0 chains into messages + UTF-8 (xyws_reassemble). The frame table comes
+    from one untimed decode with descriptors. Algorithmic bytes per call: the
+    descriptors read (32 B per frame) + payload bytes read + bytes written
+    (replies / 8 B verdicts / gathered payload + 40 B message records)."""
+    stream = torch.cuda.current_stream()
+    sp = C.c_void_p(stream.cuda_stream)
+    ctx = ws.context()
+    L, h = ctx.L, ctx.h
+    nmax = info["nframes"] + 2
+    frames_t = torch.empty(nmax * 32, dtype=torch.uint8, device="cuda")
+    n_t = torch.zeros(1, dtype=torch.int64, device="cuda")
+    assert L.xyws_decode_stream(h, C.c_void_p(buf.data_ptr()), buf.numel(), None, None,
+                                C.c_void_p(frames_t.data_ptr()), nmax, C.c_void_p(n_t.data_ptr()), 0, sp) == 0
+    torch.cuda.synchronize()
+    nf = int(n_t.item())
+    src, slen = C.c_void_p(buf.data_ptr()), buf.numel()
+    fr = C.c_void_p(frames_t.data_ptr())
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "ops.json")))["configs"].get(
+        OP_GOLDEN_KEYS.get(args.config), {})
+    plen = int(frames_t[: nf * 32].view(torch.int64).view(-1, 4)[:, 2].sum().item())
+    olen = torch.zeros(1, dtype=torch.int64, device="cuda")
+    if args.op == "encode":
+        assert L.xyws_encode_frames(h, src, slen, fr, nf, None, OP_PARAMS["enc_flags"], 0, None, None, 0, None, 0,
+                                    None, C.c_void_p(olen.data_ptr()), sp) == 0
+        torch.cuda.synchronize()
+        total = int(olen.item())
+        out = torch.empty(max(total, 1), dtype=torch.uint8, device="cuda")
+
+        def step():
+            assert L.xyws_encode_frames(h, src, slen, fr, nf, None, OP_PARAMS["enc_flags"], 0, None, None, 0,
+                                        C.c_void_p(out.data_ptr()), total, None, C.c_void_p(olen.data_ptr()), sp) == 0
+        algo = 32 * nf + plen + total
+
+        def parity():
+            g = gold.get("encode", {})
+            return int(olen.item()) == g.get("out_len") and device_digest(torch, T, out[:total]) == g.get("out_digest")
+        what = "echo replies (FIN|TEXT, unmasked) for every frame"
+    elif args.op == "classify":
+        verd = torch.zeros(max(nf, 1) * 8, dtype=torch.uint8, device="cuda")
+        first = torch.zeros(1, dtype=torch.int64, device="cuda")
+
+        def step():
+            assert L.xyws_classify_frames(h, src, slen, fr, nf, None, OP_PARAMS["cls_max_payload"],
+                                          OP_PARAMS["cls_policy"], C.c_void_p(verd.data_ptr()),
+                                          C.c_void_p(first.data_ptr()), sp) == 0
+        algo = 32 * nf + 8 * nf
+
+        def parity():
+            g = gold.get("classify", {})
+            return (device_digest(torch, T, verd[: nf * 8]) == g.get("verdicts_digest") and
+                    (int(first.item()) & ((1 << 64) - 1)) == g.get("first_close"))
+        what = "close policy per frame (FRAGMENTS, max payload 1 MiB)"
+    else:
+        out = torch.empty(max(plen, 1), dtype=torch.uint8, device="cuda")
+        msgs = torch.zeros(max(nf, 1) * 40, dtype=torch.uint8, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+
+        def step():
+            assert L.xyws_reassemble(h, src, slen, fr, nf, None, OP_PARAMS["rs_opts"], C.c_void_p(out.data_ptr()),
+                                     plen, C.c_void_p(msgs.data_ptr()), nf, C.c_void_p(cnt.data_ptr()), sp) == 0
+        algo = 32 * nf + 2 * plen + 40 * nf
+
+        def parity():
+            g = gold.get("reassemble", {})
+            nm = int(cnt.item())
+            return (nm == g.get("messages") and device_digest(torch, T, out[:plen]) == g.get("out_digest") and
+                    device_digest(torch, T, msgs[: nm * 40]) == g.get("msgs_digest"))
+        what = "FIN=0 chains into messages + UTF-8 validation"
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1) / args.steps
+    ok = bool(gold) and parity() and ctx.last_device_error() == 0
+    gbs = algo / (ms * 1e-3) / 1e9
+    print(json.dumps({
+        "metric": f"xyws {args.op} throughput (§8(f) caller, device-resident)", "op": args.op,
+        "value": round(gbs, 1), "unit": "GB/s (algorithmic bytes)", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+        "dtype": "u8", "data": "synthetic, decoded by one untimed xyws_decode_stream",
+        "config": {"workload": info["desc"], "op": what, "frames": nf, "payload_bytes": plen},
+        "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_call": algo,
+                     "kernel_ms_avg": round(ms, 4),
+                     "note": "HIP-event time per call (all of the op's kernels and launch gaps)"},
+        "parity": ok}), flush=True)
+
+
 def launch_ranks(args):
     """--gpus N without a launcher: start N ranks with torch.distributed.run as
     a CHILD process (nothing in this parent touches the GPU), pass their output
@@ -395,11 +500,71 @@ def launch_ranks(args):
     return subprocess.call(cmd)
 
 
-def dry_run(world, rank):
+def generator_frames(T, cfg_name):
+    """Frame starts of a config's generated batch as host xyws_frame records
+    (frame_off set), from the generator's own table: the host-side prefix
+    over frame sizes at generation time. Returns (records
+    as a ctypes array, n, batch bytes, payload bytes per frame)."""
+    import numpy as np
+    from xynet_amd import _lib
+    nframes, payload, b0, seed, _, _ = CONFIGS[cfg_name]
+    if nframes is not None:
+        fb = hdr_len(payload) + payload
+        offs = np.arange(nframes, dtype=np.int64) * fb
+        plens = np.full(nframes, payload, dtype=np.int64)
+        size = nframes * fb
+    else:
+        tot = C.c_uint64()
+        n = T.xyws_tools_mixed_table(seed, payload, None, 0, C.byref(tot))
+        tab = (C.c_uint8 * (32 * n))()
+        T.xyws_tools_mixed_table(seed, payload, tab, n, C.byref(tot))
+        rec = np.frombuffer(bytes(tab), dtype=np.dtype(
+            [("off", "<u8"), ("plen", "<u8"), ("draw", "<u8"), ("b0", "u1"), ("hlen", "u1"), ("pad", "u1", 6)]))
+        offs = rec["off"].astype(np.int64)
+        plens = rec["plen"].astype(np.int64)
+        size = int(tot.value)
+    recs = np.zeros((offs.size, 4), dtype=np.int64)
+    recs[:, 0] = offs
+    recs[:, 2] = plens
+    arr = (_lib.Frame * max(1, offs.size)).from_buffer_copy(recs.tobytes().ljust(32 * max(1, offs.size), b"\0"))
+    return arr, int(offs.size), size, plens, offs
+
+
+def one_batch_plan(T, cfg_name, world):
+    """--shard-one-batch: ONE config batch cut into `world` frame-aligned,
+    byte-balanced ranges (xyws_shard_plan_frames over the generator's table).
+    Returns (bounds, payload bytes per shard)."""
+    import numpy as np
+    from xynet_amd import _lib
+    arr, n, size, plens, offs = generator_frames(T, cfg_name)
+    out = (C.c_uint64 * (world + 1))()
+    rc = _lib.load().xyws_shard_plan_frames(arr, n, size, world, out)
+    assert rc == 0, rc
+    bounds = list(out)
+    idx = np.searchsorted(offs, np.array(bounds[1:-1], dtype=np.int64))
+    cuts = [0] + [int(i) for i in idx] + [n]
+    pay = [int(plens[cuts[k]:cuts[k + 1]].sum()) for k in range(world)]
+    return bounds, pay
+
+
+def dry_run(world, rank, args):
     """--dry-run: the N-rank plan without a GPU (gloo): every rank plans its
-    own shard; rank 0 prints the gathered plan (tests/test_multirank.py)."""
+    own shard; rank 0 prints the gathered plan (tests/test_multirank.py).
+    With --shard-one-batch every rank plans the cut of the one batch."""
     import torch.distributed as dist
     dist.init_process_group("gloo")
+    if args.shard_one_batch:
+        from xynet_amd import _lib
+        bounds, pay = one_batch_plan(_lib.load_tools(), args.config, world)
+        plans = [None] * world
+        dist.all_gather_object(plans, {"rank": rank, "bounds": bounds, "range": bounds[rank:rank + 2],
+                                       "payload": pay[rank]})
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "one_batch": args.config, "shards": plans}),
+                  flush=True)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     seed, gkey, desc = shard_plan("c3", rank, world)
     plans = [None] * world
     dist.all_gather_object(plans, {"rank": rank, "seed": seed, "golden": gkey})
@@ -427,6 +592,11 @@ def main():
     ap.add_argument("--stats", action="store_true", help="print fused-decoder resolution counters")
     ap.add_argument("--frames", action="store_true",
                     help="every step also returns the whole frame table and count (not the headline)")
+    ap.add_argument("--shard-one-batch", action="store_true",
+                    help="N > 1: ONE config batch cut at frame boundaries across the ranks (xyws_shard_plan_frames; "
+                         "strong scaling), instead of one independent shard per rank (config 5)")
+    ap.add_argument("--op", default="decode", choices=["decode", "encode", "classify", "reassemble"],
+                    help="time a §8(f) caller on the decoded batch instead of the decode (not the headline)")
     ap.add_argument("--xopts", type=lambda x: int(x, 0), default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -436,7 +606,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.dry_run:
-        return dry_run(world, rank)
+        return dry_run(world, rank, args)
 
     import torch
     torch.cuda.set_device(local)
@@ -447,12 +617,26 @@ def main():
 
     from xynet_amd import _lib, websocket as ws
     T = _lib.load_tools()
-    buf0, info = build_batch(torch, T, args.config, rank, world)
+    one = args.shard_one_batch
+    # --shard-one-batch: every rank holds the same (whole) batch and decodes
+    # only its frame-aligned range of it; the others' ranges are decoded after
+    # the timed region so that the whole batch's digest checks the cut
+    buf0, info = build_batch(torch, T, args.config, 0 if one else rank, 1 if one else world)
+    if args.op != "decode":
+        return op_bench(args, torch, T, ws, info, buf0)
     golden = load_golden().get(info["golden"])
+    bounds = None
+    if one:
+        bounds, pay = one_batch_plan(T, args.config, world)
+        lo_b, hi_b = bounds[rank], bounds[rank + 1]
+        info["whole_payload_bytes"] = info["payload_bytes"]
+        info["payload_bytes"] = pay[rank]
+        info["algo_bytes"] = (hi_b - lo_b) + pay[rank]
     # Batches below the 256 MiB Infinity Cache (c1, c2) are timed over >= 4
     # copies used in turn, so that each step reads its batch from HBM
     # (SURVEY.md §7); every copy's parity is checked.
-    ncopies = args.copies or (1 if info["size"] >= (1 << 30) else max(4, -(-(1 << 30) // info["size"])))
+    span = info["size"] if bounds is None else max(1, bounds[rank + 1] - bounds[rank])  # bytes one step reads
+    ncopies = args.copies or (1 if span >= (1 << 30) else max(4, -(-(1 << 30) // span)))
     bufs = [buf0] + [buf0.clone() for _ in range(ncopies - 1)]
     uses = [0] * ncopies
     dec = ws.frame_decoder(serial=(args.mode == "serial"))
@@ -467,13 +651,17 @@ def main():
         frames_t = torch.empty(max(1, info["nframes"] + 2) * 32, dtype=torch.uint8, device="cuda")
         n_t = torch.zeros(1, dtype=torch.int64, device="cuda")
 
+    def part(b, r=rank):  # the range this rank decodes
+        return b if bounds is None else b[bounds[r]:bounds[r + 1]]
+
     def step(i):  # fresh stream each step: no carry in/out (no frame table, no count by default)
         k = i % ncopies
         uses[k] += 1
+        b = part(bufs[k])
         if frames_t is None:
-            dec.decode(bufs[k], cap=0, count=False, carry=False)
+            dec.decode(b, cap=0, count=False, carry=False)
             return
-        rc = dec.ctx.L.xyws_decode_stream(dec.ctx.h, C.c_void_p(bufs[k].data_ptr()), bufs[k].numel(), None, None,
+        rc = dec.ctx.L.xyws_decode_stream(dec.ctx.h, C.c_void_p(b.data_ptr()), b.numel(), None, None,
                                           C.c_void_p(frames_t.data_ptr()), info["nframes"] + 2,
                                           C.c_void_p(n_t.data_ptr()), dec.opts, C.c_void_p(stream.cuda_stream))
         assert rc == 0, rc
@@ -528,13 +716,19 @@ def main():
 
     # parity after the timed region: every copy against the reference digest
     # for the parity of its decode count (XOR is an involution)
+    if bounds is not None:  # the other ranks' ranges, as often (mod 2) as this one's
+        for b, u in zip(bufs, uses):
+            for r in range(world):
+                if r != rank and u % 2:
+                    dec.decode(part(b, r), cap=0, count=False, carry=False)
+        torch.cuda.synchronize()
     dev_err = dec.ctx.last_device_error()
     parity = None
     if golden is not None:
         parity = dev_err == 0
         for b, u in zip(bufs, uses):
             parity = parity and device_digest(torch, T, b) == (golden["out_digest"] if u % 2 else golden["in_digest"])
-        if n_t is not None:  # the count the frame-table steps returned
+        if n_t is not None and bounds is None:  # the count the frame-table steps returned
             parity = parity and int(n_t.item()) == golden["decoded_frames"]
 
     per_gpu = args.steps * info["payload_bytes"] / t_own / GIB
@@ -542,7 +736,7 @@ def main():
     if dist:
         per_gpu_all = [None] * world
         dist.all_gather_object(per_gpu_all, round(per_gpu, 3))
-    total_payload = info["payload_bytes"] * world
+    total_payload = info["whole_payload_bytes"] if one else info["payload_bytes"] * world
     value = args.steps * total_payload / elapsed / GIB
     algo_bytes = info["algo_bytes"] + (32 * info["nframes"] if args.frames else 0)  # + the descriptors
     achieved = algo_bytes / (avg_ms * 1e-3) / 1e9
@@ -579,7 +773,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if one else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 masked frames generated in HBM; include/xyws_synth.h)",
@@ -588,10 +782,12 @@ def main():
                 "mode": args.mode + " (xyws_decode_stream: boundaries discovered on device)" +
                         (", whole frame table + count returned every step" if args.frames else ""),
                 "frames_per_gpu": info["nframes"],
-                "batch_bytes_per_gpu": info["size"],
+                "batch_bytes_per_gpu": info["size"] if bounds is None else bounds[rank + 1] - bounds[rank],
                 "payload_bytes_per_gpu": info["payload_bytes"],
                 "batch_copies": ncopies,
-                "parallelism": f"shard-by-frame x{world}, no collective",
+                "parallelism": (f"one batch cut at frame boundaries x{world} (xyws_shard_plan_frames), "
+                                f"no collective" if one else f"shard-by-frame x{world}, no collective"),
+                **({"shard_bounds": bounds} if one else {}),
             },
             "per_gpu_gibs": per_gpu_all,
             "roofline": {

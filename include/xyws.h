@@ -353,6 +353,32 @@ int xyws_notifier_destroy(xyws_notifier* n);
 int xyws_notifier_signal(xyws_notifier* n, uint64_t seq); /* marks seq complete, writes the fd */
 uint64_t xyws_notifier_completed(const xyws_notifier* n); /* highest completed seq + 1 */
 
+/* ---- one batch across several devices -----------------
+ * Frames are independent, so a batch of back-to-back frames splits across
+ * devices at frame boundaries with no exchange between them. xyws_shard_plan
+ * cuts `len` bytes of host memory (what a recv buffer_sequence holds,
+ * buffer.h:94-224 / recv_all.h:99-121 of the reference) into n_shards
+ * contiguous ranges bounds[k] .. bounds[k+1] (n_shards + 1 entries, bounds[0]
+ * = 0, bounds[n_shards] = len) balanced by bytes: bounds[k] is the frame
+ * start nearest to k * len / n_shards (each shard is within one frame of
+ * len / n_shards). Shard 0 continues from `carry_in` (nullable = a fresh
+ * stream); every other shard starts at a frame boundary, so it decodes on its
+ * own device with a fresh carry (xyws_decode_stream, dev_carry_in = NULL) to
+ * exactly the bytes and frames of the unsplit decode; only the last shard can
+ * end inside a frame (its carry out continues the stream). The headers are
+ * walked on the host (one header read per frame, parsed as
+ * websocket_frame_header_parser::parse, websocket_frame_header.h:305-385):
+ * a planner, not a decode — no payload byte is touched. A shard may be empty
+ * when one frame is larger than len / n_shards. */
+int xyws_shard_plan(const void* host_batch, uint64_t len, const xyws_carry* carry_in, uint32_t n_shards,
+                    uint64_t* bounds);
+/* The same from a frame table in host memory (frame_off ascending: e.g. the
+ * descriptors of a parse-only decode, or the table a generator or a framing
+ * layer already holds): the candidate boundaries are the frame_off >= 0
+ * values (a negative frame_off, a header carried in, is not one) and len. */
+int xyws_shard_plan_frames(const xyws_frame* frames, uint64_t n, uint64_t len, uint32_t n_shards,
+                           uint64_t* bounds);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

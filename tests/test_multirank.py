@@ -78,3 +78,39 @@ def test_bench_gpus2_launches_two_ranks_dry_run():
     assert seeds == [0x5EED0005, 0x5EED0006]
     assert sorted(p["golden"] for p in out["shards"]) == ["c5_shard0", "c5_shard1"]
     assert out["max_elapsed"] == 2.0
+
+
+@pytest.mark.parametrize("cfg,world", [("c4", 2), ("c3", 3)])
+def test_bench_shard_one_batch_dry_run(cfg, world):
+    """`bench.py --gpus N --shard-one-batch --dry-run`: ONE batch (config 4's
+    irregular frames, or config 3) cut for N ranks by xyws_shard_plan_frames
+    over the generator's table: every rank computes the same plan, the ranges
+    tile the batch, start at frames, are balanced within one frame and carry
+    the batch's whole payload. (The cut decoding to the unsplit bytes:
+    tests/test_shard.py with the oracle; on the GPU, bench.py's parity.)"""
+    import subprocess
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    from xynet_amd import _lib
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--dry-run",
+                        "--shard-one-batch", "--config", cfg], capture_output=True, text=True, timeout=300, env=env,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["n_gpus"] == world and len(out["shards"]) == world
+    bounds = out["shards"][0]["bounds"]
+    assert all(p["bounds"] == bounds for p in out["shards"])
+    _, n, size, plens, offs = bench.generator_frames(_lib.load_tools(), cfg)
+    assert bounds[0] == 0 and bounds[-1] == size and bounds == sorted(bounds)
+    starts = set(offs.tolist())
+    sizes = np.diff(np.append(offs, size))
+    for k in range(1, world):
+        assert bounds[k] in starts
+        t = size * k // world
+        i = int(np.searchsorted(offs, t, side="right")) - 1  # the frame holding the target
+        assert abs(bounds[k] - t) <= sizes[i]
+    assert sum(p["payload"] for p in out["shards"]) == int(plens.sum())

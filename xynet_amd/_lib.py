@@ -178,6 +178,10 @@ def load():
     L.xyws_notifier_signal.argtypes = [vp, u64]
     L.xyws_notifier_completed.restype = u64
     L.xyws_notifier_completed.argtypes = [vp]
+    L.xyws_shard_plan.restype = i32
+    L.xyws_shard_plan.argtypes = [vp, u64, vp, u32, C.POINTER(u64)]
+    L.xyws_shard_plan_frames.restype = i32
+    L.xyws_shard_plan_frames.argtypes = [vp, u64, u64, u32, C.POINTER(u64)]
     _lib = L
     return L
 

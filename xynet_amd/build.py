@@ -21,7 +21,7 @@ COMMON = ["--offload-arch=" + ARCH, "-O3", "-falign-loops=64", "-std=c++17", "-f
           "-Wno-unused-function", "-I" + INC, "-I" + CSRC]
 
 TARGETS = {
-    "libxyws.so": ["xyws.hip", "xyws_stream.hip", "xyws_frames.hip", "xyws_arena.hip"],
+    "libxyws.so": ["xyws.hip", "xyws_stream.hip", "xyws_frames.hip", "xyws_arena.hip", "xyws_shard.hip"],
     "libxyws_tools.so": ["xyws_tools.hip"],
 }
 DEPS = ["xyws_device.h", "xyws_stream.h", "xyws_ctx.h"]

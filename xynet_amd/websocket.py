@@ -16,6 +16,8 @@ Names, argument meaning and error behaviour follow the reference headers
   classify_frames                  websocket_check_parser_result's policy
                                    (example/include/common/websocket.h:81-108)
   reassemble                       FIN=0 chains -> messages (+ UTF-8 check)
+  shard_plan / shard_plan_frames   one batch cut at frame boundaries across devices
+                                   (a host-side header walk)
 
 Device buffers are torch uint8 tensors on a ROCm device (PyTorch is used only
 for device memory and streams). Every computing call runs HIP kernels from
@@ -455,3 +457,34 @@ class RecvArena:
             self.close()
         except Exception:
             pass
+
+
+def shard_plan(batch, n_shards, carry=None):
+    """Cut one batch of back-to-back frames (host bytes: bytes, bytearray,
+    numpy uint8 array, or a CPU uint8 tensor) into n_shards byte ranges at
+    frame boundaries, balanced by bytes (xyws_shard_plan). Returns the
+    n_shards + 1 bounds; shard k is batch[bounds[k]:bounds[k+1]], shard 0
+    continues from `carry` (a Carry or None), the others start fresh."""
+    import numpy as np
+    L = _lib.load()
+    if hasattr(batch, "numpy"):
+        batch = batch.numpy()
+    arr = np.ascontiguousarray(np.frombuffer(batch, dtype=np.uint8) if isinstance(batch, (bytes, bytearray))
+                               else batch, dtype=np.uint8)
+    out = (C.c_uint64 * (n_shards + 1))()
+    cin = C.byref(carry) if carry is not None else None
+    check(L.xyws_shard_plan(C.c_void_p(arr.ctypes.data) if arr.size else None, arr.size, cin, int(n_shards), out),
+          "xyws_shard_plan")
+    return list(out)
+
+
+def shard_plan_frames(frames, length, n_shards):
+    """shard_plan from a host frame table (a sequence of Frame, or a ctypes
+    Frame array), frame_off ascending (xyws_shard_plan_frames)."""
+    L = _lib.load()
+    n = len(frames)
+    arr = frames if isinstance(frames, C.Array) else \
+        (Frame * max(n, 1)).from_buffer_copy(b"".join(bytes(f) for f in frames).ljust(32 * max(n, 1), b"\0"))
+    out = (C.c_uint64 * (n_shards + 1))()
+    check(L.xyws_shard_plan_frames(arr, n, int(length), int(n_shards), out), "xyws_shard_plan_frames")
+    return list(out)
