@@ -160,6 +160,42 @@ def test_encode_frames_vs_oracle(ws, oracle, seed, flags, opts, with_keys, cap_f
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("src_shift", [0, 1, 5, 11, 15])
+@pytest.mark.parametrize("out_shift", [0, 3, 14])
+@pytest.mark.parametrize("short", [False, True])
+def test_encode_misaligned_and_short_source(ws, oracle, src_shift, out_shift, short):
+    """k_gather's composed chunks at every source/output alignment: the
+    decoded batch sits at src_shift in its allocation, the replies at
+    out_shift; with `short` the source handed to the encode ends inside the
+    last frames' payloads (those bytes read as zero: device error bit 0x100)."""
+    rng = streams.SplitMix(src_shift * 7 + out_shift)
+    wire = b"".join(streams.frame(rng, 0x82 if i % 3 else 0x81, n)
+                    for i, n in enumerate((0, 1, 2, 3, 5, 13, 16, 17, 31, 125, 126, 127, 300, 1000, 4099, 65536)))
+    base = torch.zeros(len(wire) + 32, dtype=torch.uint8, device="cuda")
+    t = base[src_shift:src_shift + len(wire)]
+    t.copy_(torch.frombuffer(bytearray(wire), dtype=torch.uint8))
+    dec = ws.frame_decoder()
+    r = dec.decode(t, cap=64)
+    n = r.nframes
+    host = np.frombuffer(wire, np.uint8).copy()
+    ofr, _, on = oracle.decode_stream(host, cap=64)
+    assert n == on
+    slen = len(wire) - (40000 if short else 0)
+    src = t[:slen]
+    want, offs, total = oracle.encode_frames(host[:slen].copy(), ofr, 0x11)
+    out = torch.full((total + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    view = out[out_shift:out_shift + total]
+    ws.context().last_device_error()  # (clear)
+    _, olen = ws.encode_frames(src, r.frames_t, n, 0x11, out=view)
+    torch.cuda.synchronize()
+    assert int(olen.item()) == total
+    assert view.cpu().numpy().tobytes() == want
+    assert out[:out_shift].tolist() == [0xA5] * out_shift
+    assert out[out_shift + total:].tolist() == [0xA5] * (64 - out_shift)
+    assert ws.context().last_device_error() == (0x100 if short else 0)
+
+
+@pytest.mark.gpu
 def test_encode_selected_by_verdicts_and_device_count(ws, oracle):
     """echo of DATA frames + pongs for pings, frames up to the first close only
     (dev_n = the first closing frame): classify -> encode, all on the device."""

@@ -253,34 +253,15 @@ XYWS_DEV uint8_t src_byte(const gparams& G, uint64_t p) {
 // Byte q (output coordinate) of item `it`.
 XYWS_DEV uint8_t item_byte(const gparams& G, const gitem& it, uint64_t q) {
   const uint64_t r = q - it.dst;
-  if (r < it.h) return (uint8_t)(it.hw[r >> 2] >> (8u * (r & 3u)));
+  if (r < it.h) {
+    // (shifts, not an index into hw[]: the compiler keeps it in registers)
+    const uint32_t q = (uint32_t)r;
+    const uint64_t lo = (uint64_t)it.hw[0] | ((uint64_t)it.hw[1] << 32);
+    const uint64_t hi = (uint64_t)it.hw[2] | ((uint64_t)it.hw[3] << 32);
+    return (uint8_t)((q < 8 ? lo >> (8u * q) : hi >> (8u * (q - 8))) & 0xFFu);
+  }
   const uint64_t j = r - it.h;
   return src_byte(G, it.soff + j) ^ (uint8_t)(it.key >> (8u * (j & 3u)));
-}
-
-// 16 source bytes from byte position p (any alignment; p + 16 <= src_len),
-// as four little-endian words: two aligned 16-byte loads and a funnel shift.
-XYWS_DEV void load16(const uint8_t* src, uint64_t p, uint32_t w[4]) {
-  const uint64_t a = p & ~15ull;
-  const u32x4 x = *reinterpret_cast<const u32x4*>(src + a);
-  const uint32_t sh = (uint32_t)(p & 15u);
-  if (!sh) {
-    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
-    return;
-  }
-  const u32x4 y = *reinterpret_cast<const u32x4*>(src + a + 16);
-  const uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-  const uint32_t d = sh >> 2, b = sh & 3u;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    uint32_t lo = v[0], hi = v[1];
-    // (select instead of a dynamic index into v: no scratch)
-#pragma unroll
-    for (uint32_t s = 1; s < 4; s++)
-      if (d == s) { lo = v[s + k]; hi = v[s + k + 1]; }
-    if (d == 0) { lo = v[k]; hi = v[k + 1]; }
-    w[k] = b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
-  }
 }
 
 // The last item whose output starts at or before q, among items [a, b) whose
@@ -297,8 +278,103 @@ XYWS_DEV uint64_t find_item(const uint64_t* ls, const uint64_t* off, uint64_t a,
   return lo;
 }
 
-__global__ void __launch_bounds__(FT) k_gather(gparams G) {
-  __shared__ uint64_t s_off[GLDS + 1];
+// Tile map: map[t] = the item whose output holds the first byte of gather
+// tile t (tile t covers out[] bytes [t*GTILE, (t+1)*GTILE), its first output
+// byte is q = max(t*GTILE - out_lo, 0)). One lane per item writes the tiles
+// whose first byte it holds (a 1 MiB reply spans 64 of them), so a tile finds
+// its items with one load instead of a binary search of the offsets.
+__global__ void __launch_bounds__(FT) k_tile_map(gparams G, uint64_t* map, uint64_t ntiles) {
+  const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
+  const uint64_t ne = n_eff(G.n, G.dev_n);
+  if (i >= ne) return;
+  const uint64_t total = G.off[ne];
+  const uint64_t lim = total < G.out_cap ? total : G.out_cap;
+  const uint64_t qs = G.off[i], qe0 = G.off[i + 1], qe = qe0 < lim ? qe0 : lim;
+  if (qs >= qe) return;
+  if (qs == 0) map[0] = i;
+  uint64_t t = (qs + G.out_lo + GTILE - 1) / GTILE;
+  if (t == 0) t = 1;
+  const uint64_t t1 = (qe + G.out_lo + GTILE - 1) / GTILE;
+  for (; t < t1 && t < ntiles; t++) map[t] = i;
+}
+
+// Bytes [e, e + 16) of the 16-byte little-endian vector h placed at offset 0
+// of an otherwise zero byte line (e in [-15, 15]; bytes outside h read 0).
+XYWS_DEV u32x4 window16(const uint32_t h[4], int32_t e) {
+  const uint32_t v[12] = {0u, 0u, 0u, 0u, h[0], h[1], h[2], h[3], 0u, 0u, 0u, 0u};
+  const uint32_t s = (uint32_t)(16 + e), d = s >> 2, b = s & 3u;
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t lo = 0u, hi = 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++)
+      if (d == j) { lo = v[j + k]; hi = v[j + k + 1]; }
+    w[k] = b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
+  }
+  return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+// Byte-select mask (per dword, 0xFF per byte) of the chunk bytes t in [lo, hi)
+// (chunk-relative, may lie outside [0, 16)).
+XYWS_DEV u32x4 span_mask(int64_t lo, int64_t hi) {
+  uint32_t m[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int64_t a = 4 * k;
+    const int64_t l = lo > a ? (lo - a < 4 ? lo - a : 4) : 0;
+    const int64_t h = hi > a ? (hi - a < 4 ? hi - a : 4) : 0;
+    const uint32_t mh = h >= 4 ? 0xFFFFFFFFu : ((1u << (8u * (uint32_t)h)) - 1u);
+    const uint32_t ml = l >= 4 ? 0xFFFFFFFFu : ((1u << (8u * (uint32_t)l)) - 1u);
+    m[k] = h > l ? (mh & ~ml) : 0u;
+  }
+  return u32x4{m[0], m[1], m[2], m[3]};
+}
+
+// 16 source bytes at src offset p (signed, may start before 0 or run past the
+// end): the two aligned 16-byte lines around it, lines outside the source
+// [0, round16(src_lo + src_len)) read as zero.
+XYWS_DEV u32x4 src16(const gparams& G, int64_t p) {
+  const int64_t A = (int64_t)G.src_lo + p;
+  const int64_t a = A & ~(int64_t)15;
+  const int64_t top = (int64_t)((G.src_lo + G.src_len + 15) & ~15ull);
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  const u32x4 x = (a >= 0 && a < top) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(G.src + a)) : z;
+  const uint32_t sh = (uint32_t)(A & 15);
+  if (!sh) return x;
+  const u32x4 y = (a + 16 >= 0 && a + 16 < top) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(G.src + a + 16)) : z;
+  const uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+  const uint32_t d = sh >> 2, b = sh & 3u;
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t lo = v[k], hi = v[k + 1];
+#pragma unroll
+    for (uint32_t s = 1; s < 4; s++)
+      if (d == s) { lo = v[s + k]; hi = v[s + k + 1]; }
+    w[k] = b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
+  }
+  return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+// Items staged per tile (struct of arrays in LDS).
+struct gstage {
+  uint64_t dst[GLDS + 1];  // output start (q coordinate); dst[k] of the item after the last: its start
+  uint64_t soff[GLDS];
+  uint32_t hw[GLDS][4];
+  uint32_t h[GLDS], key[GLDS];
+};
+
+// The gather (encode replies / message payloads): output tiles of GTILE bytes,
+// each lane four 16-byte chunks. The items touching a tile (from the tile map)
+// are staged in LDS once; a chunk finds its first item by a binary search in
+// LDS and is composed from at most a few items: header bytes from the staged
+// header words, payload bytes from two aligned 16-byte source loads and a
+// funnel shift, XORed with the rotated key word, each selected by its byte
+// mask. One 16-byte store per chunk (byte stores only at the output's ends).
+// Tiles with more items than fit in LDS take the per-byte path.
+__global__ void __launch_bounds__(FT) k_gather(gparams G, const uint64_t* __restrict__ map, uint64_t ntiles) {
+  __shared__ gstage S;
   __shared__ uint64_t s_f0, s_f1;
   const uint64_t ne = n_eff(G.n, G.dev_n);
   const uint64_t total = G.off[ne];
@@ -307,41 +383,39 @@ __global__ void __launch_bounds__(FT) k_gather(gparams G) {
   // output chunks are 16-byte aligned in the out[] coordinate: q in [0, lim)
   // sits at out_lo + q
   const uint64_t o0 = G.out_lo, o1 = G.out_lo + lim;
-  const uint64_t ntiles = (o1 + GTILE - 1) / GTILE;
-  for (uint64_t tile = blockIdx.x + (o0 / GTILE); tile < ntiles; tile += gridDim.x) {
-    const uint64_t t0 = tile * GTILE, t1 = t0 + GTILE;
-    const uint64_t q0 = t0 > o0 ? t0 - o0 : 0, q1 = (t1 < o1 ? t1 : o1) - o0;  // output range of the tile
+  const uint64_t nt = (o1 + GTILE - 1) / GTILE;
+  for (uint64_t tile = blockIdx.x; tile < nt && tile < ntiles; tile += gridDim.x) {
+    const uint64_t t0 = tile * GTILE;
     if (threadIdx.x == 0) {
-      s_f0 = find_item(nullptr, G.off, 0, ne, 0, q0);
-      s_f1 = find_item(nullptr, G.off, 0, ne, 0, q1 - 1) + 1;  // items [f0, f1) touch the tile
+      s_f0 = map[tile];
+      s_f1 = tile + 1 < nt ? map[tile + 1] + 1 : ne;
+      if (s_f1 > ne) s_f1 = ne;
     }
     __syncthreads();
     const uint64_t f0 = s_f0, f1 = s_f1;
     const bool in_lds = f1 - f0 <= GLDS;
-    if (in_lds)
-      for (uint64_t k = threadIdx.x; k <= f1 - f0; k += FT) s_off[k] = G.off[f0 + k];
+    if (in_lds) {
+      for (uint64_t k = threadIdx.x; k < f1 - f0; k += FT) {
+        const gitem it = item_of(G, f0 + k);
+        S.dst[k] = it.dst;
+        S.soff[k] = it.soff;
+        S.hw[k][0] = it.hw[0]; S.hw[k][1] = it.hw[1]; S.hw[k][2] = it.hw[2]; S.hw[k][3] = it.hw[3];
+        S.h[k] = it.h;
+        S.key[k] = it.key;
+      }
+      if (threadIdx.x == 0) S.dst[f1 - f0] = G.off[f1];
+    }
     __syncthreads();
 #pragma unroll 1
     for (uint32_t c = 0; c < GTILE / 16 / FT; c++) {
       const uint64_t a = t0 + (uint64_t)(c * FT + threadIdx.x) * 16;  // aligned out[] position
       if (a + 16 <= o0 || a >= o1) continue;
       const uint64_t qa = a > o0 ? a - o0 : 0;  // first output byte of the chunk
-      const uint64_t g = find_item(in_lds ? s_off : nullptr, G.off, f0, f1, f0, qa);
-      gitem it = item_of(G, g);
-      const uint64_t ps = it.dst + it.h, pe = ps + it.len;  // payload part of the item
-      uint32_t w[4];
-      if (a >= o0 && a + 16 <= o1 && a - o0 >= ps && a - o0 + 16 <= pe &&
-          it.soff + (a - o0 - ps) + 16 <= G.src_len) {
-        // the whole chunk is payload of one item: 16 source bytes
-        const uint64_t j = a - o0 - ps;
-        load16(G.src, G.src_lo + it.soff + j, w);
-        const uint32_t kw = rotr8(it.key, (uint32_t)j);
-        w[0] ^= kw; w[1] ^= kw; w[2] ^= kw; w[3] ^= kw;
-        *reinterpret_cast<u32x4*>(G.out + a) = u32x4{w[0], w[1], w[2], w[3]};
-      } else {
-        // headers, item boundaries, edges: byte by byte
-        uint64_t gi = g;
-        uint64_t nxt = gi + 1 < ne ? (in_lds && gi + 1 - f0 <= GLDS ? s_off[gi + 1 - f0] : G.off[gi + 1]) : U64MAX;
+      if (!in_lds) {
+        // many tiny items: byte by byte from memory
+        uint64_t gi = find_item(nullptr, G.off, f0, f1, f0, qa);
+        gitem it = item_of(G, gi);
+        uint64_t nxt = gi + 1 < ne ? G.off[gi + 1] : U64MAX;
         for (uint32_t t = 0; t < 16; t++) {
           const uint64_t p = a + t;
           if (p < o0 || p >= o1) continue;
@@ -352,6 +426,55 @@ __global__ void __launch_bounds__(FT) k_gather(gparams G) {
             nxt = gi + 1 < ne ? G.off[gi + 1] : U64MAX;
           }
           G.out[p] = item_byte(G, it, q);
+        }
+        continue;
+      }
+      const uint32_t n = (uint32_t)(f1 - f0);
+      uint32_t g = 0;
+      {
+        uint32_t hi = n;
+        while (hi - g > 1) {
+          const uint32_t m = (g + hi) >> 1;
+          if (S.dst[m] <= qa) g = m; else hi = m;
+        }
+      }
+      const int64_t ca = (int64_t)a - (int64_t)o0;  // q of chunk byte 0 (may be < 0 in the first chunk)
+      u32x4 w = {0u, 0u, 0u, 0u};
+      bool oob = false;
+      for (uint32_t k = g; k < n && (int64_t)S.dst[k] < ca + 16; k++) {
+        const int64_t ds = (int64_t)S.dst[k], de = (int64_t)S.dst[k + 1];
+        const int64_t ps = ds + S.h[k];
+        if (S.h[k] && ds < ca + 16 && ps > ca) {  // header bytes
+          uint32_t hw[4] = {S.hw[k][0], S.hw[k][1], S.hw[k][2], S.hw[k][3]};
+          const u32x4 v = window16(hw, (int32_t)(ca - ds));
+          const u32x4 m = span_mask(ds - ca, ps - ca);
+          w |= v & m;
+        }
+        if (de > ps && ps < ca + 16 && de > ca) {  // payload bytes
+          const int64_t d = ca - ps;  // payload index of chunk byte 0
+          const int64_t sp = (int64_t)S.soff[k] + d;
+          u32x4 v = src16(G, sp);
+          const uint32_t kw = rotr8(S.key[k], (uint32_t)d);
+          const u32x4 m = span_mask(ps - ca, de - ca);
+          // bytes past the source read as zero (and are reported)
+          const int64_t past = (int64_t)G.src_len - sp;  // chunk bytes t >= past lie past src_len
+          if (past < 16) {
+            const u32x4 vm = span_mask(past, 16);
+            v &= ~vm;
+            const u32x4 pm = vm & m;
+            if (pm.x | pm.y | pm.z | pm.w) oob = true;
+          }
+          w |= (v ^ kw) & m;
+        }
+      }
+      if (oob) atomicOr(G.err, 0x100u);
+      if (a >= o0 && a + 16 <= o1) {
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(G.out + a));
+      } else {
+        for (uint32_t t = 0; t < 16; t++) {
+          const uint64_t p = a + t;
+          const uint32_t wt = t < 4 ? w.x : t < 8 ? w.y : t < 12 ? w.z : w.w;  // (no dynamic index: no scratch)
+          if (p >= o0 && p < o1) G.out[p] = (uint8_t)(wt >> (8u * (t & 3u)));
         }
       }
     }
@@ -599,11 +722,14 @@ int xyws_encode_frames(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, con
   if (rc) return rc;
   // scratch: offsets (n + 1, unless the caller's), block partials, total
   const uint64_t nb = (n + SB - 1) / SB + 1;
-  if ((rc = ensure_aux(sl, 8 * ((dev_offsets ? 0 : n + 1) + nb + 2), capt))) return rc;
+  const uint64_t oa0 = reinterpret_cast<uintptr_t>(dev_out) & 15;
+  const uint64_t ntiles = (oa0 + out_cap + GTILE - 1) / GTILE + 1;
+  if ((rc = ensure_aux(sl, 8 * ((dev_offsets ? 0 : n + 1) + nb + 2 + ntiles), capt))) return rc;
   uint64_t* aux = static_cast<uint64_t*>(sl->aux_mem);
   uint64_t* off = dev_offsets ? dev_offsets : aux;
   uint64_t* part = dev_offsets ? aux : aux + n + 1;
   uint64_t* total = part + nb;
+  uint64_t* tmap = total + 2;
   const uintptr_t oa = reinterpret_cast<uintptr_t>(dev_out);
   const uintptr_t sa = reinterpret_cast<uintptr_t>(dev_src);
   gparams G;
@@ -632,7 +758,8 @@ int xyws_encode_frames(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, con
   }
   if (n && out_cap) {
     const uint64_t tiles = (G.out_lo + out_cap + GTILE - 1) / GTILE;
-    hipLaunchKernelGGL(k_gather, dim3(grid_for(tiles, 1, 8192)), dim3(FT), 0, s, G);
+    hipLaunchKernelGGL(k_tile_map, dim3((n + FT - 1) / FT), dim3(FT), 0, s, G, tmap, ntiles);
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(tiles, 1, 8192)), dim3(FT), 0, s, G, (const uint64_t*)tmap, ntiles);
     if ((rc = hip_err(hipGetLastError()))) return rc;
   }
   return XYWS_OK;
@@ -672,11 +799,13 @@ int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, const 
   // scratch: a, b, st/rank, sz/off, cnt/cntoff, orphan flags/prefix (n + 1
   // each), block partials, totals
   const uint64_t w = n + 1, nb = (n + SB - 1) / SB + 1;
-  if ((rc = ensure_aux(sl, 8 * (6 * w + nb + 4), capt))) return rc;
+  const uint64_t ntiles = ((reinterpret_cast<uintptr_t>(dev_out) & 15) + out_cap + GTILE - 1) / GTILE + 1;
+  if ((rc = ensure_aux(sl, 8 * (6 * w + nb + 4 + ntiles), capt))) return rc;
   uint64_t* A = static_cast<uint64_t*>(sl->aux_mem);
   uint64_t *a = A, *b = A + w, *st = A + 2 * w, *off = A + 3 * w, *cnt = A + 4 * w, *orph = A + 5 * w;
   uint64_t* part = A + 6 * w;
   uint64_t* tot = part + nb;  // tot[0]: bytes, tot[1]: messages, tot[2], tot[3]: scratch totals
+  uint64_t* tmap = tot + 4;   // gather tile map
   if ((rc = hip_err(hipMemsetAsync(orph, 0, 8 * w, s)))) return rc;
   const dim3 gn((uint32_t)((n + FT - 1) / FT > 0 ? (n + FT - 1) / FT : 1));
   if (n) {
@@ -723,7 +852,8 @@ int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, const 
   G.err = ctx->err;
   if (n && out_cap) {
     const uint64_t tiles = (G.out_lo + out_cap + GTILE - 1) / GTILE;
-    hipLaunchKernelGGL(k_gather, dim3(grid_for(tiles, 1, 8192)), dim3(FT), 0, s, G);
+    hipLaunchKernelGGL(k_tile_map, dim3((n + FT - 1) / FT), dim3(FT), 0, s, G, tmap, ntiles);
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(tiles, 1, 8192)), dim3(FT), 0, s, G, (const uint64_t*)tmap, ntiles);
     if ((rc = hip_err(hipGetLastError()))) return rc;
   }
   if ((opts & XYWS_REASM_UTF8) && out_cap && msg_cap) {
