@@ -144,9 +144,12 @@ const char* xyws_strerror(int code);
 /* Bind a context to HIP device `device`. One context per (thread, device). */
 int xyws_ctx_create(int device, xyws_ctx** out);
 int xyws_ctx_destroy(xyws_ctx* ctx);
-/* Pre-size scratch for batches up to `max_batch_bytes` (and, for indexed mode,
- * `max_frames` caller starts) so that later calls allocate nothing and can be
- * captured into a hipGraph. Calls on larger batches grow scratch lazily. */
+/* Pre-size scratch for batches up to `max_batch_bytes` (and, for indexed mode
+ * and frame descriptors, `max_frames` frames) so that later calls allocate
+ * nothing and can be captured into a hipGraph. The per-frame tables go to the
+ * streams already used on the context, and to a new stream at its first
+ * uncaptured call (make one before capturing on it). Calls on larger
+ * batches grow scratch lazily. */
 int xyws_ctx_reserve(xyws_ctx* ctx, uint64_t max_batch_bytes, uint64_t max_frames);
 /* Device-side error word of the last completed call (0 = none). Synchronizes
  * the context's device. */
@@ -313,7 +316,9 @@ int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len,
  * here, or the caller's buffer registered with hipHostRegister, e.g. the
  * memory an io_uring registered-buffer ring hands to recv), a device mirror,
  * a device-resident carry and up to XYWS_ARENA_SLOTS submissions in flight on
- * the arena's own HIP stream. xyws_arena_submit(offset, len) enqueues
+ * one of the context's arena streams (arenas share 8 streams round robin, so
+ * any number of connections binds at most 8 scratch slots; an arena's
+ * submissions stay in order). xyws_arena_submit(offset, len) enqueues
  * H2D -> xyws_decode_stream (carry chained across submissions, so a frame cut
  * by a recv boundary decodes as if unsplit) -> D2H of the unmasked bytes back
  * into the same host range (in place, like websocket_mask) and of the frame
@@ -326,6 +331,10 @@ int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len,
  * poll() or wait() returned them: submit() returns XYWS_ERR_AGAIN while
  * XYWS_ARENA_SLOTS submissions are in flight or unclaimed. */
 #define XYWS_ARENA_SLOTS 8
+/* A submit that fails before anything was enqueued leaves the arena as it
+ * was; one that fails later (the decode or a copy back could not be
+ * enqueued) leaves it failed: the device carry may have moved past bytes no
+ * result reports, so every later submit returns XYWS_ERR_HIP (destroy it). */
 typedef struct xyws_arena xyws_arena;
 typedef struct xyws_arena_result {
   uint64_t seq;              /* the submission */

@@ -264,6 +264,28 @@ def test_reassemble_vs_oracle(ws, oracle, seed, cap_frac):
     if cap_frac == 1.0:
         got = [(r[5], out[r[2]:r[2] + r[3]].cpu().numpy().tobytes()) for r in _messages(mt, nm) if r[4] & 1]
         assert got == msgs  # every complete message, as the generator wrote it
+    ws.context().last_device_error()  # (clears bit 0x200: this stream may end in orphan continuations)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [3, 8])
+def test_reassemble_small_msg_cap_and_trailing_orphans(ws, oracle, seed):
+    """msg_cap below the message count: every stored record is the oracle's
+    (the last one ends at the next message's start, not at the batch end);
+    continuations after the last message set bit 0x200 of the error word."""
+    from xynet_amd import _lib
+    rng = streams.SplitMix(seed)
+    wire, _ = msg_streams.message_stream(seed, nmsg=60)
+    wire += msg_streams._frame(rng, 0x82, rng.bytes(10))  # a whole message (closes any open one)...
+    wire += msg_streams._frame(rng, 0x80, rng.bytes(30))  # ...then an orphan continuation, no message after it
+    t, frames_t, n, host, ofr = _decode(ws, oracle, wire)
+    oout, orecs = oracle.reassemble(host, ofr, _lib.REASM_UTF8)
+    for cap in (1, len(orecs) // 2, len(orecs) - 1):
+        ws.context().last_device_error()  # (clear)
+        out, mt, cnt = ws.reassemble(t, frames_t, n, _lib.REASM_UTF8, msg_cap=cap)
+        assert int(cnt.item()) == len(orecs)
+        assert _messages(mt, cap) == [r.as_tuple() for r in orecs[:cap]]
+        assert ws.context().last_device_error() == 0x200
 
 
 @pytest.mark.gpu

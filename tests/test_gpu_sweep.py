@@ -265,3 +265,47 @@ def test_sweep_stats_show_no_repairs_on_c3(ws):
     assert out[_lib.ST_SW_DEFER] <= 1024, list(out)
     del buf, r
     torch.cuda.empty_cache()
+
+
+def _policy(dec):
+    out = (C.c_uint64 * 5)()
+    stream = torch.cuda.current_stream()
+    assert dec.ctx.L.xyws_debug_policy(dec.ctx.h, C.c_void_p(stream.cuda_stream), out) == 0
+    return list(out)
+
+
+def test_decoder_choice_follows_the_frames(ws):
+    """The decoder choice (stream_decode_fused: sweep_preferred): a call
+    without descriptors takes the sweep decoder when the previous call on the
+    stream found regular frames of 16 KiB or more (config 3), the run decoder
+    otherwise (config 4's irregular frames, config 2's 256 B ones). Every call
+    is checked against the reference's digests, whichever decoder ran."""
+    from xynet_amd import _lib
+    seq = [("c3_bin_64k", 0), ("c3_bin_64k", 0), ("c3_bin_64k", 0), ("c4_mixed", 0), ("c4_mixed", 0),
+           ("c2_bin_256", 0), ("c2_bin_256", 0), ("c3_bin_64k", _lib.OPT_RUNS)]
+    dec = ws.frame_decoder()
+    used, pols = [], []
+    bufs = {}
+    for name, extra in seq:
+        if name not in bufs:
+            bufs.clear()
+            torch.cuda.empty_cache()
+            bufs[name] = [tools_batch(name), 0]
+        (buf, c), k = bufs[name]
+        dec.opts = extra
+        r = dec.decode(buf, cap=0, count=True, carry=False)
+        bufs[name][1] = k + 1
+        assert r.nframes == c["decoded_frames"], name
+        assert dev_digest(buf) == (c["out_digest"] if (k + 1) % 2 else c["in_digest"]), (name, k)
+        assert dec.ctx.last_device_error() == 0
+        p = _policy(dec)
+        used.append(p[4])
+        pols.append(p)
+    # c3: regular 64 KiB frames (65 550 B with the header)
+    assert pols[0][2] == pols[0][3] == 65550
+    assert used[1] == 1 and used[2] == 1          # the sweep after a regular large-frame call
+    assert used[3] == 1                           # the first c4 call follows c3's statistics...
+    assert pols[3][2] < pols[3][3]                # ...and finds irregular frames
+    assert used[4] == 0                           # so the next one takes the run decoder
+    assert pols[5][2] == pols[5][3] == 264 and used[6] == 0  # 256 B frames: runs
+    assert used[7] == 0                           # XYWS_OPT_RUNS forces the run decoder

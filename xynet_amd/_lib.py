@@ -25,6 +25,7 @@ OPT_STEAL = 0x400000
 OPT_TEST_STEAL = 0x800000
 OPT_SWEEP = 0x1000000      # the sweep decoder (segment claiming) instead of the run decoder
 OPT_TEST_SPEC = 0x2000000  # sweep decoder tests: forced mis-speculation
+OPT_RUNS = 0x80000000      # the run decoder whatever the decoder choice would take
 # debug stats indices (xyws_stream.hip)
 ST_RUNS, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRAMES = range(8)
 ST_GIVEUP, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS = 32, 33, 34, 35, 36
@@ -135,6 +136,8 @@ def load():
     L.xyws_decode_indexed.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp]
     L.xyws_debug_stats.restype = i32
     L.xyws_debug_stats.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
+    L.xyws_debug_policy.restype = i32
+    L.xyws_debug_policy.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
     L.xyws_debug_records.restype = C.c_int64
     L.xyws_debug_records.argtypes = [vp, vp, C.POINTER(C.c_uint64), u64]
     L.xyws_decode_stream.restype = i32

@@ -297,6 +297,8 @@ int xyws_ctx_create(int device, xyws_ctx** out) {
   c->reserve_frames = 0;
   c->stage = nullptr;
   c->stage_cap = 0;
+  for (auto& st : c->arena_stream) st = nullptr;
+  c->arena_rr = 0;
   for (auto& sl : c->slot) {
     sl.bound = false;
     sl.stream = nullptr;
@@ -310,7 +312,7 @@ int xyws_ctx_create(int device, xyws_ctx** out) {
     delete c;
     return XYWS_ERR_NOMEM;
   }
-  if (hipMemset(c->err, 0, 64) != hipSuccess) {
+  if (zero_now(c->err, 64) != hipSuccess) {
     (void)hipFree(c->err);
     delete c;
     return XYWS_ERR_HIP;
@@ -331,6 +333,8 @@ int xyws_ctx_destroy(xyws_ctx* ctx) {
     }
     if (ctx->err) (void)hipFree(ctx->err);
     if (ctx->stage) (void)hipFree(ctx->stage);
+    for (auto st : ctx->arena_stream)
+      if (st) (void)hipStreamDestroy(st);
   }
   delete ctx;
   return XYWS_OK;
@@ -344,15 +348,14 @@ int xyws_ctx_reserve(xyws_ctx* ctx, uint64_t max_batch_bytes, uint64_t max_frame
   if (max_batch_bytes > ctx->reserve_bytes) ctx->reserve_bytes = max_batch_bytes;
   if (max_frames > ctx->reserve_frames) ctx->reserve_frames = max_frames;
   for (auto& sl : ctx->slot) {
-    if (ctx->reserve_frames) {
-      int rc = ensure_table(&sl, ctx->reserve_frames, false);
-      if (rc) return rc;
-    }
+    // the stream decoder's scratch (small: ~160 B per 128 KiB segment) in
+    // every slot; the per-frame tables only in slots bound to a stream now
+    // (the others get them when a stream binds them: acquire_slot)
     int rc = stream_scratch_reserve(&sl.ss, ctx->reserve_bytes);
     if (rc) return rc;
-    if (ctx->reserve_frames) {
-      rc = stream_scratch_reserve_frames(&sl.ss, ctx->reserve_bytes, ctx->reserve_frames);
-      if (rc) return rc;
+    if (ctx->reserve_frames && sl.bound) {
+      if ((rc = ensure_table(&sl, ctx->reserve_frames, false))) return rc;
+      if ((rc = stream_scratch_reserve_frames(&sl.ss, ctx->reserve_bytes, ctx->reserve_frames))) return rc;
     }
   }
   return XYWS_OK;
@@ -365,7 +368,7 @@ int xyws_ctx_last_device_error(xyws_ctx* ctx, uint32_t* out) {
   if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
   uint32_t v = 0;
   if (hipMemcpy(&v, ctx->err, 4, hipMemcpyDeviceToHost) != hipSuccess) return XYWS_ERR_HIP;
-  if (v && hipMemset(ctx->err, 0, 4) != hipSuccess) return XYWS_ERR_HIP;
+  if (v && zero_now(ctx->err, 4) != hipSuccess) return XYWS_ERR_HIP;
   for (auto& sl : ctx->slot) v |= stream_scratch_error(&sl.ss, true);
   *out = v;
   return v ? XYWS_ERR_DEVICE : XYWS_OK;
@@ -392,6 +395,23 @@ int64_t xyws_debug_records(xyws_ctx* ctx, void* stream, uint64_t* out, uint64_t 
   device_guard g(ctx->device);
   for (auto& sl : ctx->slot)
     if (sl.bound && sl.stream == (hipStream_t)stream) return stream_scratch_records(&sl.ss, out, max_runs);
+  return XYWS_ERR_INVALID;
+}
+
+// Internal: the decoder-choice words the last fused stream decode on `stream`
+// published ({epoch, batch bytes, smallest, largest last-frame size, decoder:
+// 0 runs / 1 sweep}). Synchronizes the device.
+int xyws_debug_policy(xyws_ctx* ctx, void* stream, uint64_t* out) {
+  if (!ctx || !out) return XYWS_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  device_guard g(ctx->device);
+  if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
+  for (auto& sl : ctx->slot)
+    if (sl.bound && sl.stream == (hipStream_t)stream) {
+      if (!sl.ss.pol_h) return XYWS_ERR_INVALID;
+      for (int i = 0; i < 5; i++) out[i] = sl.ss.pol_h[i];
+      return XYWS_OK;
+    }
   return XYWS_ERR_INVALID;
 }
 
@@ -603,7 +623,7 @@ int xyws_parser_reset(xyws_parser* p) {
   p->fed = 0;
   p->finished = false;
   memset(&p->res, 0, sizeof p->res);
-  return hip_err(hipMemset(p->dev, 0, 64));  // a zero carry: a fresh parser (s_start)
+  return hip_err(zero_now(p->dev, 64));  // a zero carry: a fresh parser (s_start)
 }
 
 int xyws_parser_parse(xyws_parser* p, const void* data, uint64_t len, uint64_t* consumed, void* stream) {

@@ -72,6 +72,7 @@ struct xyws_arena {
   xyws_carry* dev_carry;
   xyws_notifier note;
   uint64_t next_seq;
+  bool failed;  // a submission failed after work was enqueued: every later submit fails
   arena_slot slot[XYWS_ARENA_SLOTS];
   arena_cb cb[XYWS_ARENA_SLOTS];
 };
@@ -95,7 +96,7 @@ void arena_free(xyws_arena* a) {
   if (a->dev_carry) (void)hipFree(a->dev_carry);
   if (a->host && a->owned) (void)hipHostFree(a->host);
   if (a->host && a->registered) (void)hipHostUnregister(a->host);
-  if (a->stream) (void)hipStreamDestroy(a->stream);
+  // (the stream is the context's: arena_stream)
   delete a;
 }
 
@@ -155,10 +156,17 @@ int xyws_arena_create(xyws_ctx* ctx, void* host, uint64_t bytes, uint64_t max_fr
   a->note.fd = eventfd;
   a->note.completed.store(0);
   a->next_seq = 0;
+  a->failed = false;
   int rc = XYWS_OK;
-  if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) {
-    a->stream = nullptr;
-    rc = XYWS_ERR_HIP;
+  {
+    // one of the context's arena streams, round robin (created on first use)
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    hipStream_t& st = ctx->arena_stream[ctx->arena_rr++ % XYWS_ARENA_STREAMS];
+    if (!st && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+      st = nullptr;
+      rc = XYWS_ERR_HIP;
+    }
+    a->stream = st;
   }
   if (!rc) {
     if (host) {
@@ -172,7 +180,7 @@ int xyws_arena_create(xyws_ctx* ctx, void* host, uint64_t bytes, uint64_t max_fr
   }
   if (!rc && hipMalloc(&a->dev, bytes + 64) != hipSuccess) { a->dev = nullptr; rc = XYWS_ERR_NOMEM; }
   if (!rc && hipMalloc(&a->dev_carry, sizeof(xyws_carry)) != hipSuccess) { a->dev_carry = nullptr; rc = XYWS_ERR_NOMEM; }
-  if (!rc && hipMemset(a->dev_carry, 0, sizeof(xyws_carry)) != hipSuccess) rc = XYWS_ERR_HIP;
+  if (!rc && zero_now(a->dev_carry, sizeof(xyws_carry)) != hipSuccess) rc = XYWS_ERR_HIP;
   for (auto& s : a->slot) {
     if (rc) break;
     s.seq = ~0ull;
@@ -204,34 +212,42 @@ int xyws_arena_submit(xyws_arena* a, uint64_t offset, uint64_t len, uint32_t opt
   if (!a || offset > a->bytes || len > a->bytes - offset) return XYWS_ERR_INVALID;
   // a slot is free once the results of the submission that used it were
   // taken (poll / wait): results stay valid until then
+  if (a->failed) return XYWS_ERR_HIP;
   const uint64_t s_no = a->next_seq;
   arena_slot& s = a->slot[s_no % XYWS_ARENA_SLOTS];
   if (!s.consumed) return XYWS_ERR_AGAIN;
   device_guard g(a->ctx->device);
   if (!g.ok) return XYWS_ERR_HIP;
+  hipStream_t st = a->stream;
+  uint8_t* dv = a->dev + offset;
+  // nothing enqueued yet: a failure here leaves the arena as it was
+  if (len && hipMemcpyAsync(dv, a->host + offset, len, hipMemcpyHostToDevice, st) != hipSuccess) return XYWS_ERR_HIP;
+  // from here on the device carry may move: a failure leaves the arena failed
+  // (no result would report the bytes it passed; the caller destroys it)
+  int rc = xyws_decode_stream(a->ctx, dv, len, a->dev_carry, a->dev_carry, s.dev_frames, a->max_frames,
+                              s.dev_count, opts & ~XYWS_OPT_SERIAL_SCAN, st);
+  if (!rc && len && !(opts & XYWS_OPT_PARSE_ONLY) &&
+      hipMemcpyAsync(a->host + offset, dv, len, hipMemcpyDeviceToHost, st) != hipSuccess)
+    rc = XYWS_ERR_HIP;
+  if (!rc && (hipMemcpyAsync(s.host_meta, s.dev_count, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+              hipMemcpyAsync(s.host_meta + 8, a->dev_carry, sizeof(xyws_carry), hipMemcpyDeviceToHost, st) !=
+                  hipSuccess ||
+              hipMemcpyAsync(s.host_frames, s.dev_frames, a->max_frames * sizeof(xyws_frame),
+                             hipMemcpyDeviceToHost, st) != hipSuccess))
+    rc = XYWS_ERR_HIP;
+  arena_cb& c = a->cb[s_no % XYWS_ARENA_SLOTS];
+  c.n = &a->note;
+  c.seq = s_no;
+  if (!rc && hipLaunchHostFunc(st, on_complete, &c) != hipSuccess) rc = XYWS_ERR_HIP;
+  if (rc) {
+    a->failed = true;
+    return rc;
+  }
+  // the slot is taken once every enqueue succeeded
   s.seq = s_no;
   s.consumed = false;
   s.offset = offset;
   s.len = len;
-  hipStream_t st = a->stream;
-  uint8_t* dv = a->dev + offset;
-  int rc = XYWS_OK;
-  if (len && hipMemcpyAsync(dv, a->host + offset, len, hipMemcpyHostToDevice, st) != hipSuccess) return XYWS_ERR_HIP;
-  rc = xyws_decode_stream(a->ctx, dv, len, a->dev_carry, a->dev_carry, s.dev_frames, a->max_frames, s.dev_count,
-                          opts & ~XYWS_OPT_SERIAL_SCAN, st);
-  if (rc) return rc;
-  if (len && !(opts & XYWS_OPT_PARSE_ONLY) &&
-      hipMemcpyAsync(a->host + offset, dv, len, hipMemcpyDeviceToHost, st) != hipSuccess)
-    return XYWS_ERR_HIP;
-  if (hipMemcpyAsync(s.host_meta, s.dev_count, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipMemcpyAsync(s.host_meta + 8, a->dev_carry, sizeof(xyws_carry), hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipMemcpyAsync(s.host_frames, s.dev_frames, a->max_frames * sizeof(xyws_frame), hipMemcpyDeviceToHost, st) !=
-          hipSuccess)
-    return XYWS_ERR_HIP;
-  arena_cb& c = a->cb[s_no % XYWS_ARENA_SLOTS];
-  c.n = &a->note;
-  c.seq = s_no;
-  if (hipLaunchHostFunc(st, on_complete, &c) != hipSuccess) return XYWS_ERR_HIP;
   a->next_seq = s_no + 1;
   if (seq) *seq = s_no;
   return XYWS_OK;

@@ -48,7 +48,13 @@ struct xyws_ctx {
   void* stage;          // xyws_mask_bytes: device copy of host bytes (under mu)
   uint64_t stage_cap;
   scratch_slot slot[XYWS_SLOTS];
+  // recv arenas share a few streams of the context (arena k: stream k mod
+  // XYWS_ARENA_STREAMS), so that any number of connections bind at most that
+  // many scratch slots (created on first use, destroyed with the context)
+  hipStream_t arena_stream[8];
+  uint32_t arena_rr;
 };
+#define XYWS_ARENA_STREAMS 8
 
 namespace xyws_internal {
 
@@ -65,6 +71,16 @@ struct device_guard {
 };
 
 inline int hip_err(hipError_t e) { return e == hipSuccess ? XYWS_OK : XYWS_ERR_HIP; }
+
+// Zero device memory and wait until it is zero: hipMemset on device memory may
+// return before the memset ran (it goes to the null stream, which does not
+// order the caller's non-blocking streams); a kernel on such a stream would
+// otherwise read the allocation's old contents (scratch tickets, epochs).
+inline hipError_t zero_now(void* p, size_t n) {
+  hipError_t e = hipMemset(p, 0, n);
+  if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+  return e;
+}
 
 inline bool capturing(hipStream_t s) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -122,6 +138,12 @@ inline int acquire_slot(xyws_ctx* ctx, hipStream_t stream, bool capture, scratch
     }
     for (auto& sl : ctx->slot)
       if (!sl.bound) { pick = &sl; break; }
+  }
+  if (!pick->bound && ctx->reserve_frames && !capture) {
+    // xyws_ctx_reserve's per-frame tables go to the slots streams bind (not
+    // to all XYWS_SLOTS up front: tens of GB for 2^26 frames)
+    if (const int rc = ensure_table(pick, ctx->reserve_frames, false)) return rc;
+    if (const int rc = stream_scratch_reserve_frames(&pick->ss, ctx->reserve_bytes, ctx->reserve_frames)) return rc;
   }
   pick->bound = true;
   pick->stream = stream;

@@ -581,15 +581,19 @@ __global__ void __launch_bounds__(FT) k_rs_sizes(const xyws_frame* frames, uint6
   cnt[i] = c;
 }
 
-// message records: first_frame by rank (st[] exclusive-scanned = ranks)
+// message records: first_frame by rank (st[] exclusive-scanned = ranks);
+// starts[m] = the first frame of message m for EVERY message (also past
+// msg_cap: a record's length and frame count end at the next message's start)
 __global__ void __launch_bounds__(FT) k_rs_first(const xyws_frame* frames, uint64_t n, const uint64_t* dev_n,
-                                                 const uint64_t* rank, xyws_message* msgs, uint64_t msg_cap) {
+                                                 const uint64_t* rank, uint64_t* starts, xyws_message* msgs,
+                                                 uint64_t msg_cap) {
   const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
   const uint64_t ne = n_eff(n, dev_n);
   if (i >= ne) return;
   const uint32_t op = frames[i].flags & XYWS_FLAG_OP_MASK;
   if (op != XYWS_FLAG_OP_TEXT && op != XYWS_FLAG_OP_BINARY) return;
   const uint64_t m = rank[i];
+  starts[m] = i;
   if (m < msg_cap) {
     msgs[m].first_frame = i;
     msgs[m].opcode = (uint8_t)op;
@@ -597,17 +601,24 @@ __global__ void __launch_bounds__(FT) k_rs_first(const xyws_frame* frames, uint6
 }
 
 // the rest of each record from the offsets of its start and the next start
+// (starts[]: every message's first frame, k_rs_first); continuations after
+// the last message's FIN with no message after them set bit 0x200 of the
+// device error word
 __global__ void __launch_bounds__(FT) k_rs_msgs(const uint64_t* dev_n, uint64_t n, const uint64_t* nmsg_p,
                                                 const uint64_t* off, const uint64_t* cntoff, const uint64_t* b,
-                                                const uint64_t* orphan, const uint64_t* orph_rank,
+                                                const uint64_t* starts, const uint64_t* orph_rank,
                                                 uint64_t out_cap, xyws_message* msgs, uint64_t msg_cap,
-                                                uint64_t* dev_nmsgs) {
+                                                uint64_t* dev_nmsgs, uint32_t* err) {
   const uint64_t m = (uint64_t)blockIdx.x * FT + threadIdx.x;
   const uint64_t ne = n_eff(n, dev_n), nm = *nmsg_p;
-  if (m == 0 && dev_nmsgs) *dev_nmsgs = nm;
+  if (m == 0) {
+    if (dev_nmsgs) *dev_nmsgs = nm;
+    const uint64_t before = nm ? orph_rank[starts[nm - 1]] : 0;
+    if (orph_rank[ne] > before) atomicOr(err, 0x200u);
+  }
   if (m >= nm || m >= msg_cap) return;
-  const uint64_t s = msgs[m].first_frame;
-  const uint64_t ns = m + 1 < nm && m + 1 < msg_cap ? msgs[m + 1].first_frame : ne;
+  const uint64_t s = starts[m];
+  const uint64_t ns = m + 1 < nm ? starts[m + 1] : ne;
   msgs[m].out_off = off[s];
   msgs[m].length = off[ns] - off[s];
   msgs[m].nframes = cntoff[ns] - cntoff[s];
@@ -618,9 +629,8 @@ __global__ void __launch_bounds__(FT) k_rs_msgs(const uint64_t* dev_n, uint64_t 
   // orphans between the previous start (or the batch start) and this one:
   // orph_rank = orphan flags prefix-summed; orphans before s minus those
   // before the previous start
-  const uint64_t ps = m ? msgs[m - 1].first_frame : 0;
+  const uint64_t ps = m ? starts[m - 1] : 0;
   if (orph_rank[s] - (m ? orph_rank[ps] : 0) > 0) st |= XYWS_MSG_ORPHANS;
-  (void)orphan;
   msgs[m].status = st;
   msgs[m].reserved[0] = msgs[m].reserved[1] = msgs[m].reserved[2] = 0;
 }
@@ -824,13 +834,14 @@ int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, const 
   if ((rc = scan<op_sum, false, true>(st, n, part, tot + 1, s))) return rc;
   if ((rc = scan<op_sum, false, true>(orph, n, part, tot + 3, s))) return rc;
   if (n) {
-    hipLaunchKernelGGL(k_rs_first, gn, dim3(FT), 0, s, dev_frames, n, dev_n, (const uint64_t*)st, dev_msgs,
+    // (a[] is free after k_rs_sizes: every message's first frame)
+    hipLaunchKernelGGL(k_rs_first, gn, dim3(FT), 0, s, dev_frames, n, dev_n, (const uint64_t*)st, a, dev_msgs,
                        msg_cap);
     if ((rc = hip_err(hipGetLastError()))) return rc;
   }
   hipLaunchKernelGGL(k_rs_msgs, gn, dim3(FT), 0, s, dev_n, n, (const uint64_t*)(tot + 1), (const uint64_t*)off,
-                     (const uint64_t*)cnt, (const uint64_t*)b, (const uint64_t*)orph, (const uint64_t*)orph,
-                     out_cap, dev_msgs, msg_cap, dev_nmsgs);
+                     (const uint64_t*)cnt, (const uint64_t*)b, (const uint64_t*)a, (const uint64_t*)orph,
+                     out_cap, dev_msgs, msg_cap, dev_nmsgs, ctx->err);
   if ((rc = hip_err(hipGetLastError()))) return rc;
   const uintptr_t oa = reinterpret_cast<uintptr_t>(dev_out);
   const uintptr_t sa = reinterpret_cast<uintptr_t>(dev_src);

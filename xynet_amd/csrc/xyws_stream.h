@@ -16,6 +16,12 @@ struct stream_scratch {
   void* smem;           // sweep decoder: per-segment granules, records and flag bitmap
   uint64_t sbytes;
   uint64_t max_segs;    // segments smem covers
+  // decoder choice: pinned host words the finisher of every call writes
+  // ({epoch, batch bytes, smallest, largest last-frame size, decoder}) and
+  // their device address; null when the pinned allocation failed (then the
+  // run decoder serves every call that does not ask for the sweep)
+  volatile uint64_t* pol_h;
+  uint64_t* pol_d;
 };
 
 void stream_scratch_init(stream_scratch* s, int device);
@@ -48,6 +54,7 @@ int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_ru
 #define XYWS_OPT_SWX_NOVAL 0x10000000u  // timing experiments only (wrong results possible): no deferred checks
 #define XYWS_OPT_SWX_NOREC 0x20000000u  // timing experiments only: no segment records
 #define XYWS_OPT_SW_LOADWAIT 0x40000000u  // experiment (sweep): the next segment's loads land before the stores issue
+#define XYWS_OPT_RUNS 0x80000000u     // the run decoder, whatever the decoder choice would take
 #define XYWS_OPT_TEST_SPEC 0x2000000u  // tests (sweep decoder): segments 1, 4, 7, ... report no entry, segments
                                        // 2, 5, 8, ... speculate one byte late (look-back fix-ups, repair walk)
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,

@@ -57,6 +57,7 @@
 
 #include "xyws_stream.h"
 #include "xyws_device.h"
+#include "xyws_ctx.h"  // (zero_now)
 
 namespace {
 
@@ -191,6 +192,10 @@ constexpr uint32_t HW_DONE = 64, HW_BAD = 65, HW_TOTAL = 66, HW_FINAL = 67;
 constexpr uint32_t HW_EMIT_SLOW = 73;
 // ...copied by finish_call for k_stream_emit (and reset there)
 constexpr uint32_t HW_EMIT_FLAG = 74;
+// decoder choice (stream_decode_fused): the largest and (complemented) the
+// smallest size of the last frame of every run / segment exit of the call,
+// published by the finisher into the context's host-visible policy slot
+constexpr uint32_t HW_FSMAX = 75, HW_FSMIN = 76;
 
 XYWS_DEV void granule_store(uint64_t* g, uint64_t a, uint64_t b) {
   const u32x4 v = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
@@ -257,6 +262,9 @@ struct run_params {
   uint64_t* sgran;
   uint64_t* srec;
   uint64_t* sbits;
+  // host-visible policy slot (device address of pinned host memory; nullable):
+  // written by the workgroup that finishes the call (pol_publish)
+  uint64_t* pol;
 };
 
 template <class G>
@@ -301,6 +309,7 @@ struct __attribute__((aligned(16))) lds_t {
   cstate sw_spec, sw_in, sw_vU;
   uint32_t sw_act, sw_single, sw_cnt_spec, sw_fast, sw_padok;
   uint64_t sw_t[9];  // sweep timing split (XYWS_OPT_STATS): see ST_SWT_*
+  uint64_t sw_fsmin, sw_fsmax;  // lane 0: smallest / largest last-frame size of the segments decoded
 };
 
 // ---------------------------------------------------------------- small helpers
@@ -318,6 +327,31 @@ enum { ST_RUNS = 0, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRA
        ST_GIVEUP = 32, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS, ST_D_TVAL, ST_T_ROWS, ST_T_SER };
 XYWS_DEV void stat_add(const run_params& P, uint32_t i, uint64_t v) {
   if (stats_on(P)) atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + i, (unsigned long long)v);
+}
+
+// The size of the frame a chain state last completed (H + P), for the
+// decoder choice: 0 when the state holds no whole frame of this batch.
+XYWS_DEV uint64_t last_frame_size(const cstate& S);
+// Lane 0 of a run or segment: fold a last-frame size into the call's min/max.
+XYWS_DEV void fs_note(const run_params& P, uint64_t fsmin, uint64_t fsmax) {
+  uint64_t* hw = reinterpret_cast<uint64_t*>(P.head);
+  if (!fsmax) return;
+  __hip_atomic_fetch_max(hw + HW_FSMAX, fsmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_max(hw + HW_FSMIN, ~fsmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The finisher (lane 0): the call's frame-size range into the host-visible
+// policy slot {epoch, batch bytes, smallest, largest last-frame size, decoder}
+// and the words reset for the next call. Host memory: system-scope stores.
+XYWS_DEV void pol_publish(const run_params& P, uint64_t E, uint64_t decoder) {
+  uint64_t* hw = reinterpret_cast<uint64_t*>(P.head);
+  const uint64_t mx = st_load(hw + HW_FSMAX), mn = ~st_load(hw + HW_FSMIN);
+  st_store(hw + HW_FSMAX, 0);
+  st_store(hw + HW_FSMIN, 0);
+  if (!P.pol) return;
+  const uint64_t v[5] = {E, P.hi - P.lo, mx ? mn : 0, mx, decoder};
+#pragma unroll
+  for (int i = 1; i < 5; i++) __hip_atomic_store(P.pol + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(P.pol, v[0], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 XYWS_DEV uint32_t clamp_rel(uint64_t x, uint64_t ss) {
@@ -355,6 +389,11 @@ XYWS_DEV cstate frame_state(uint64_t start, const hdr_info& h) {
   s.st = 0;
   s.pad = 0;
   return s;
+}
+
+XYWS_DEV uint64_t last_frame_size(const cstate& S) {
+  const bool whole = !(S.st & (S_NOCOV | S_PARTIAL | S_PARTCARRY | S_CARRIED | S_HDRCARRY | S_CUT));
+  return (whole && S.X > S.cov_start && S.X != ~0ull) ? S.X - S.cov_start : 0;
 }
 
 // ---------------------------------------------------------------- header reads
@@ -1958,6 +1997,10 @@ XYWS_DEV void decode_range(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint
     if (!ok) __hip_atomic_fetch_or(hw + HW_BAD, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (L.cnt) __hip_atomic_fetch_add(hw + HW_TOTAL, L.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ok && L.succ >= P.nflat) put_state(hw + HW_FINAL, L.S);
+    if (L.cnt) {
+      const uint64_t fs = last_frame_size(L.S);
+      fs_note(P, fs, fs);
+    }
     if (stats_on(P)) st_store(rec + R_T2, __builtin_amdgcn_s_memrealtime());
     if (!ok) stat_add(P, ST_BAD, 1);
     if (L.tmo) stat_add(P, ST_GIVEUP, 1);
@@ -2376,6 +2419,7 @@ __device__ __attribute__((noinline)) void finish_call(run_params P, lds_t<G>& L,
       st_store(hw + HW_EMIT_FLAG, (walked || st_load(hw + HW_EMIT_SLOW)) ? 1u : 0u);
       st_store(hw + HW_EMIT_SLOW, 0);
     }
+    pol_publish(P, L.E, 0);
     st_store(hw + HW_BAD, 0);
     st_store(hw + HW_TOTAL, 0);
     st_store(hw + HW_DONE, 0);
@@ -3348,11 +3392,6 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
       const bool any = !(P.opts & XYWS_OPT_NO_STORE) && wl_r < wh_r;
       build_rows<G>(L, L.nfl, 0u, G::SEG, wl_r, wh_r, any, tid);
     }
-    const uint64_t vs = L.sw_vs;
-    if (vs != NONE && !(P.opts & XYWS_OPT_SWX_NOVAL)) {
-      sweep_validate(P, vs, vs * G::SEG, E, tid, L.sw_vU);
-      if (tid == 0) L.sw_vs = NONE;
-    }
     if (tid == 0 && stats_on(P)) L.sw_t[2] += __builtin_amdgcn_s_memtime() - tb0;
   }
   __syncthreads();
@@ -3397,6 +3436,15 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
       store_rows<G, ROLE == SWR_ALL>(P, L, ss, tid, act == SW_REUSE ? L.nfl : 0u, act == SW_REUSE ? G::SEG : 0u, wl,
                                      whi, wl_r, wh_r);
     if (tid == 64 && stats_on(P)) L.sw_t[5] += __builtin_amdgcn_s_memtime() - ts0;
+    // the control wave checks the previous predicted segment while the data
+    // waves store (its look-back waits for memory: off the stores' path)
+    if (CT && tid < 64) {
+      const uint64_t vs = L.sw_vs;
+      if (vs != NONE && !(P.opts & XYWS_OPT_SWX_NOVAL)) {
+        sweep_validate(P, vs, vs * G::SEG, E, tid, L.sw_vU);
+        if (tid == 0) L.sw_vs = NONE;
+      }
+    }
   }
   __syncthreads();
   uint64_t cnt = 0;
@@ -3427,6 +3475,13 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
                      F.X > F.cov_start && fs <= XCLAMP;
     L.sw_ref = ref ? F.X : NONE;
     L.sw_fsz = ref ? fs : 0;
+    if (cnt) {  // (the decoder choice: the workgroup's range of last-frame sizes)
+      const uint64_t lf = last_frame_size(F);
+      if (lf) {
+        if (lf > L.sw_fsmax) L.sw_fsmax = lf;
+        if (lf < L.sw_fsmin) L.sw_fsmin = lf;
+      }
+    }
     if (act == SW_APPLY) stat_add(P, ST_SW_APPLY, 1);
     if (!fast) stat_add(P, ST_SW_DEFER, 1);
     if (mode != SWM_PRED && mode != SWM_EXACT0) stat_add(P, ST_SW_WIN, 1);
@@ -3542,6 +3597,7 @@ XYWS_DEV void sweep_finish(const run_params& P, lds_t<G>& L, uint32_t tid) {
 #pragma unroll
     for (int i = 0; i < 8; i++) reinterpret_cast<uint64_t*>(&L.cinc)[i] = c[i];
     write_outputs(P, &L.cinc, total, S);
+    pol_publish(P, L.E, 1);
     st_store(hw + HW_BAD, 0);
     st_store(hw + HW_TOTAL, 0);
     st_store(hw + HW_DONE, 0);
@@ -3617,6 +3673,8 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_sweep(run_params P) {
     L.sw_pcur = NONE;
     L.sw_fcur = 0;
     L.sw_vs = NONE;
+    L.sw_fsmin = ~0ull;
+    L.sw_fsmax = 0;
 #pragma unroll
     for (int i = 0; i < 9; i++) L.sw_t[i] = 0;
   }
@@ -3644,6 +3702,7 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_sweep(run_params P) {
   if (tid0 == 0 && frames)
     __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(P.head) + HW_TOTAL, frames, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+  if (tid0 == 0) fs_note(P, L.sw_fsmin, L.sw_fsmax);
   // end of the workgroup: the finisher may re-read any segment's stored bytes
   // (the repair walk), so every storing wave drains, then an agent-scope
   // release before the done-count add and an acquire in the finisher
@@ -3729,12 +3788,28 @@ void stream_scratch_init(stream_scratch* s, int device) {
   s->fmem = nullptr;
   s->fbytes = 0;
   s->ncu = 256;
+  s->pol_h = nullptr;
+  s->pol_d = nullptr;
+  void* ph = nullptr;
+  if (hipHostMalloc(&ph, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+    void* pd = nullptr;
+    memset(ph, 0, 64);
+    if (hipHostGetDevicePointer(&pd, ph, 0) == hipSuccess) {
+      s->pol_h = static_cast<volatile uint64_t*>(ph);
+      s->pol_d = static_cast<uint64_t*>(pd);
+    } else {
+      (void)hipHostFree(ph);
+    }
+  }
   int n = 0;
   if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && n > 0)
     s->ncu = n;
 }
 
 void stream_scratch_free(stream_scratch* s) {
+  if (s->pol_h) (void)hipHostFree(const_cast<uint64_t*>(s->pol_h));
+  s->pol_h = nullptr;
+  s->pol_d = nullptr;
   if (s->smem) (void)hipFree(s->smem);
   s->smem = nullptr;
   s->sbytes = 0;
@@ -3791,7 +3866,7 @@ static int scratch_grow(stream_scratch* s, uint64_t runs) {
   s->mem = m;
   s->bytes = bytes;
   s->max_runs = want;
-  return hipMemset(m, 0, records_off(want)) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
+  return xyws_internal::zero_now(m, records_off(want)) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
 
 // Sweep decoder scratch for up to `segs` segments: entry granules (32 B per
@@ -3814,7 +3889,7 @@ static int sweep_grow(stream_scratch* s, uint64_t segs, bool capturing) {
   s->smem = m;
   s->sbytes = bytes;
   s->max_segs = want;
-  return hipMemset(m, 0, zb) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
+  return xyws_internal::zero_now(m, zb) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
 
 int stream_scratch_reserve_frames(stream_scratch* s, uint64_t max_batch_bytes, uint64_t max_frames) {
@@ -3856,8 +3931,26 @@ uint32_t stream_scratch_error(stream_scratch* s, bool clear) {
   if (!s->mem) return 0;
   uint32_t v[2] = {0, 0};
   if (hipMemcpy(v, s->mem, 8, hipMemcpyDeviceToHost) != hipSuccess) return 0xFFFFFFFFu;
-  if (clear && v[1] && hipMemset(static_cast<uint8_t*>(s->mem) + 4, 0, 4) != hipSuccess) return 0xFFFFFFFFu;
+  if (clear && v[1] && xyws_internal::zero_now(static_cast<uint8_t*>(s->mem) + 4, 4) != hipSuccess) return 0xFFFFFFFFu;
   return v[1];
+}
+
+// The decoder choice for a call without descriptors, from what the previous
+// call on this scratch (this stream) found (the policy words its finisher
+// wrote; read without waiting for it: a value one call old at most matters
+// for speed only). The sweep decoder (segments claimed from one counter:
+// every CU streams to the end of the batch) is faster when the frames are
+// large and regular, so that each segment's entry follows from the stride of
+// the frames before it (c3 / c5: 64 KiB frames, profiles/r03*); the run
+// decoder (one contiguous range per CU, one entry scan per run) is faster on
+// small frames (its dense pass) and on irregular ones (no stride to follow).
+// Regular: every run's or segment's last frame has the same size. Both
+// decoders are exact on any bytes.
+constexpr uint64_t SWEEP_MIN_FRAME = 16384;
+static bool sweep_preferred(const stream_scratch* s, uint64_t len) {
+  if (!s->pol_h || len < (64ull << 20)) return false;
+  const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
+  return fsmax && fsmin == fsmax && fsmin >= SWEEP_MIN_FRAME;
 }
 
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
@@ -3871,11 +3964,13 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   hipStreamCaptureStatus cs0 = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(stream, &cs0);
   const bool capt = cs0 != hipStreamCaptureStatusNone;
-  // The sweep decoder takes a call that asks for it, no descriptors and none
-  // of the run decoder's own modes.
+  // The sweep decoder takes a call that asks for it, or that the decoder
+  // choice gives it (sweep_preferred), with no descriptors and none of the
+  // run decoder's own modes.
   constexpr uint32_t RUN_MODES = XYWS_OPT_PARSE_ONLY | XYWS_OPT_WG512 | XYWS_OPT_DIAG | XYWS_OPT_TEST_GIVEUP |
-                                 XYWS_OPT_STEAL | XYWS_OPT_TEST_STEAL;
-  if ((opts & XYWS_OPT_SWEEP) && !(frames && cap) && !(opts & RUN_MODES)) {
+                                 XYWS_OPT_STEAL | XYWS_OPT_TEST_STEAL | XYWS_OPT_RUNS;
+  const bool want_sweep = (opts & XYWS_OPT_SWEEP) || (!small && sweep_preferred(s, hi - lo));
+  if (want_sweep && !(frames && cap) && !(opts & RUN_MODES)) {
     const uint64_t seg = small ? G_SWEEP_SMALL::SEG : G_SWEEP::SEG;
     const uint64_t nseg = (hi + seg - 1) / seg;
     if (!s->mem) {  // (the head words: claim counter, epoch, end-of-call words)
@@ -3897,6 +3992,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     P.sgran = reinterpret_cast<uint64_t*>(sm);
     P.sbits = reinterpret_cast<uint64_t*>(sm + sweep_gran_bytes(s->max_segs));
     P.srec = reinterpret_cast<uint64_t*>(sm + sweep_gran_bytes(s->max_segs) + sweep_bits_bytes(s->max_segs));
+    P.pol = s->pol_d;
     if ((opts & XYWS_OPT_STATS) && hipMemsetAsync(m + 128, 0, 8 * XYWS_NSTATS, stream) != hipSuccess) return XYWS_ERR_HIP;
     const uint64_t maxg = small ? 64 : (uint64_t)s->ncu;
     const uint32_t grid = (uint32_t)(nseg < maxg ? nseg : maxg);
@@ -3944,6 +4040,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   P.cin_user = cin;
   P.cin = reinterpret_cast<xyws_carry*>(m + 64);
   P.fst = nullptr; P.rcap = 0;
+  P.pol = s->pol_d;
   if (frames && cap) {
     const uint64_t rc_n = region_entries(cap, nruns);
     const int rc = fmem_grow(s, 8 * (uint64_t)P.nflat * rc_n, cs != hipStreamCaptureStatusNone);
