@@ -690,6 +690,11 @@ def main():
     t1 = time.perf_counter()
     elapsed = max_over_ranks(dist, torch, t1 - t0, "cuda")
     avg_ms = ev0.elapsed_time(ev1) / args.steps
+    decoder = None  # which decoder served the timed steps (the decoder choice, xyws_stream.hip)
+    if args.mode == "fused":
+        pol = (C.c_uint64 * 5)()
+        if dec.ctx.L.xyws_debug_policy(dec.ctx.h, C.c_void_p(stream.cuda_stream), pol) == 0:
+            decoder = ["runs (k_stream_runs)", "sweep (k_stream_sweep)"][int(pol[4]) & 1]
 
     if args.stats and rank == 0:  # two extra decodes of copy 0 (keeps its parity)
         names = ["runs", "runs_without_entry", "bad_boundaries", "repairs", "cuts", "spins", "dense_passes",
@@ -779,6 +784,7 @@ def main():
             "data": "synthetic (splitmix64 masked frames generated in HBM; include/xyws_synth.h)",
             "config": {
                 "workload": info["desc"],
+                "decoder": decoder,
                 "mode": args.mode + " (xyws_decode_stream: boundaries discovered on device)" +
                         (", whole frame table + count returned every step" if args.frames else ""),
                 "frames_per_gpu": info["nframes"],
@@ -800,8 +806,8 @@ def main():
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "kernel_ms_avg": round(avg_ms, 4),
-                "kernel_ms_note": "HIP-event time per decode over the timed steps (runs + finish kernels "
-                                  "and the gaps between steps); per-kernel split: profiles/*_kernel_stats.csv",
+                "kernel_ms_note": "HIP-event time per decode over the timed steps (the decoder kernel, its "
+                                  "in-kernel finish and the gaps between steps); per-kernel: profiles/*_kernel_stats.csv",
                 "src_sha": source_hash(),
                 "copy_ceiling": ceiling,
             },

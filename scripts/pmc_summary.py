@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 PMC passes of the bench into profiles/pmc_traffic.json.
 
-HBM traffic per k_stream_runs launch (the dominant kernel of xyws_decode_stream), per MI355X_MICROARCH.md §HBM: gfx950's
+HBM traffic per launch of the decoder kernel the timed steps ran (k_stream_sweep or k_stream_runs), per MI355X_MICROARCH.md §HBM: gfx950's
 FETCH_SIZE reports half the bytes of wide coalesced streaming reads (doubled
 here); WRITE_SIZE reads the bytes exactly for 16-B-per-lane stores. Both
 counters are in KiB. Usage: pmc_summary.py FETCH_DIR WRITE_DIR KEY PROFILE [OUT]
@@ -15,15 +15,25 @@ import os
 import sys
 
 
-def per_launch(d, counter, kernel="k_stream_runs"):
-    vals = []
+def per_launch(d, counter, kernel=None):
+    """Average counter value per launch of `kernel` (a name substring); by
+    default the decoder kernel (k_stream_runs / k_stream_sweep) with the most
+    launches in the pass, i.e. the one the timed steps ran (the decoder
+    choice may serve the first warm-up call with the other one)."""
+    vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
-                vals.append(float(r["Counter_Value"]))
+            name = r["Kernel_Name"]
+            hit = (kernel in name) if kernel else ("k_stream_runs" in name or "k_stream_sweep" in name)
+            if hit and r["Counter_Name"] == counter:
+                k = "k_stream_sweep" if "k_stream_sweep" in name else ("k_stream_runs" if "k_stream_runs" in name
+                                                                        else kernel)
+                vals.setdefault(k, []).append(float(r["Counter_Value"]))
     if not vals:
-        raise SystemExit(f"no {counter} rows for {kernel} under {d}")
-    return sum(vals) / len(vals), len(vals)
+        raise SystemExit(f"no {counter} rows for {kernel or 'the decoder kernels'} under {d}")
+    k = max(vals, key=lambda x: len(vals[x]))
+    v = vals[k]
+    return sum(v) / len(v), len(v), k
 
 
 def source_hash():
@@ -40,9 +50,11 @@ def main():
     fdir, wdir, key, profile = sys.argv[1:5]
     out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
-    fk, nf = per_launch(fdir, "FETCH_SIZE")
-    wk, nw = per_launch(wdir, "WRITE_SIZE")
+    fk, nf, kf = per_launch(fdir, "FETCH_SIZE")
+    wk, nw, kw = per_launch(wdir, "WRITE_SIZE")
+    assert kf == kw, (kf, kw)
     rec = {
+        "kernel": kf,
         "fetch_size_kib_raw": fk, "write_size_kib": wk, "launches": [nf, nw],
         "hbm_read_bytes_per_launch": int(fk * 2 * 1024),
         "hbm_write_bytes_per_launch": int(wk * 1024),

@@ -302,6 +302,7 @@ struct __attribute__((aligned(16))) lds_t {
   uint32_t dent[G::NSB], dcnt[G::NSB], dexit[G::NSB], doff[G::NSB];
   uint4 dlast[G::NSB];
   uint32_t dense;  // frames of the previous pass (the dense pass is tried after a dense one)
+  uint32_t sgood;  // the stride pass serves dense segments (cleared when it did not cover one)
   uint32_t nrec;   // descriptors requested: frame starts the current item recorded
   // sweep decoder: claimed segments (current, next, claimed ahead), the spec
   // entry and state, the entering state from the look-back, decisions
@@ -810,6 +811,92 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   L.pass_hi = seg_done ? G::SEG : (uint32_t)((S.X - ss) & ~15ull);
 }
 
+// Stride pass (wave 0, every lane; the first pass of a segment, before lane
+// 0's serial chase). In a stream of equal frames the frame after X starts at
+// X + F, F the size of the frame that ends at X; lane i parses the header at
+// X + i*F from LDS (the serial chase's 32-bit parse, below the same stop).
+// Lane 0's position is exact (X); lane i's is exact when lanes 0..i-1 each
+// found a frame of exactly F bytes (induction from X), so ONE ballot accepts
+// lanes 0..m, m the first lane whose frame is not F bytes long (its start is
+// exact too; its own size ends the step). A step decides up to 64 frames in
+// one LDS round trip where the serial chase takes one hop per frame, and it
+// is exact whatever the bytes: no accepted position is a guess. Steps repeat
+// from the new X while one accepts STRIDE_MIN frames or more. Returns the
+// list entries written (the covering frame first, as chase_pass writes it;
+// 0: nothing accepted, the list untouched) and leaves L.S, L.cnt and the
+// descriptor starts as chase_pass would: lane 0's serial chase continues
+// from there (limits, the segment end, lengths of 2^31 or more).
+constexpr uint32_t STRIDE_MIN = 8;
+template <class G>
+XYWS_DEV uint32_t stride_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t lane) {
+  const cstate S0 = L.S;
+  const uint64_t se = ss + G::SEG;
+  const bool known = L.known != 0, past = L.past != 0;
+  const bool dense_seg = L.dense >= 2 * G::NSB;
+  if (past || S0.st != 0 || S0.X < ss || S0.X >= se || S0.X <= S0.cov_start) return 0;
+  const uint64_t F = S0.X - S0.cov_start;
+  if (F < 2 || F > G::SEG / STRIDE_MIN) return 0;
+  // chase_pass's fast-path stop: headers wholly in LDS, in the batch, below
+  // the write limit, before the successor's entry
+  const uint64_t lim = known ? L.Wn : NONE;
+  uint64_t fstop = se - XYWS_MAX_FRAME_HEADER_SIZE + 1;
+  const uint64_t hlim = P.hi < lim ? P.hi : lim;
+  if (hlim < fstop + XYWS_MAX_FRAME_HEADER_SIZE - 1)
+    fstop = hlim >= XYWS_MAX_FRAME_HEADER_SIZE - 1 ? hlim - (XYWS_MAX_FRAME_HEADER_SIZE - 1) : 0;
+  if (known && L.hn < fstop) fstop = L.hn;
+  if (S0.X >= fstop) return 0;
+  const uint64_t st = fstop - ss;
+  // the covering frame's entry (chase_pass: when it reaches into the segment)
+  const uint32_t n0 = S0.X > ss ? 1u : 0u;
+  if (lane == 0 && n0) L.fl[0] = fent{0u, clamp_rel(S0.cov_ps, ss), clamp_rel(S0.X, ss), S0.cov_kw};
+  uint32_t n = n0, total = 0, x = (uint32_t)(S0.X - ss), f = (uint32_t)F;
+  cstate S = S0;
+  for (;;) {
+    const uint64_t p64 = (uint64_t)x + (uint64_t)lane * f;
+    const bool valid = p64 < st && n + lane < G::FCAP;
+    const uint32_t p = (uint32_t)p64;
+    uint32_t hl = 0, plen = 0, key = 0, b01 = 0;
+    bool ok = false;
+    if (valid) ok = parse_rel<G>(L, p, hl, plen, key, b01);
+    const uint64_t vm = __ballot(valid), okm = __ballot(ok), mm = __ballot(ok && hl + plen == f);
+    const uint32_t m = mm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~mm);  // first lane without a match
+    uint32_t a = (m < 64 && ((okm >> m) & 1ull)) ? m + 1 : m;
+    const uint32_t nv = (uint32_t)__builtin_popcountll(vm);  // (valid lanes are 0..nv-1)
+    if (a > nv) a = nv;
+    if (a == 0) break;
+    if (lane < a) {
+      const uint32_t ps = p + hl;
+      L.fl[n + lane] = fent{p, ps, ps + plen, rotr8(key, 0u - ps)};
+    }
+    // the last accepted frame is the chain state
+    const uint32_t l = a - 1;
+    const uint32_t lp = __builtin_amdgcn_readlane(p, l), lhl = __builtin_amdgcn_readlane(hl, l);
+    const uint32_t lpl = __builtin_amdgcn_readlane(plen, l), lkey = __builtin_amdgcn_readlane(key, l);
+    S.cov_start = ss + lp;
+    S.cov_ps = ss + lp + lhl;
+    S.X = ss + lp + lhl + lpl;
+    S.cov_key = lkey;
+    S.cov_kw = rotr8(lkey, 0u - (lp + lhl));
+    S.st = 0;
+    n += a;
+    total += a;
+    x = lp + lhl + lpl;
+    f = lhl + lpl;
+    if (a < STRIDE_MIN || x >= st || n >= G::FCAP) break;
+  }
+  if (lane == 0) {
+    if (total) {
+      L.S = S;
+      L.cnt += total;
+      if (P.fst) record_starts<G>(P, L, ss, n0, total);
+    }
+    // (a segment the dense pass would take and this pass did not cover: the
+    // dense pass from the next segment on)
+    if (dense_seg && total < 2 * G::NSB) L.sgood = 0;
+  }
+  return total ? n : 0u;
+}
+
 // Dense pass (many small frames): the segment's chase split over NSB
 // sub-blocks of SB bytes (entries searched by 16 lanes each, chased by one
 // lane each of wave 0), chased at once. Sub-block 0 starts
@@ -1083,6 +1170,61 @@ XYWS_DEV void build_rows(lds_t<G>& L, uint32_t nfl, uint32_t lo_c, uint32_t hi_c
   }
 }
 
+// Chunks of the rows that are neither FAST nor SKIP (a frame boundary lies in
+// the row), in a lane-private pass before the store loop (not unrolled: few
+// registers live while the next segment's loads are in flight). Each of this
+// lane's such chunks in [lo_c, hi_c) and wholly inside the write window [wl_r,
+// wh_r) gets the words of every frame it overlaps XORed into its LDS copy
+// (header bytes XOR 0: they stay as parsed) and bit k of the result: the store
+// loop then stores it as it is, in the same instruction as its neighbours, so
+// every line is written once (boundary chunks stored on their own after the
+// loop wrote their lines a second time: c2 wrote 1.33x its batch). A chunk
+// that crosses the window's edge gets bit k of `edge` (the byte path after
+// the store loop). chunk_of(k, a, r, ok): the lane's k-th chunk offset, its
+// 1 KiB row, and whether it exists.
+template <class G, uint32_t NK, class ChunkOf>
+XYWS_DEV uint32_t boundary_chunks(lds_t<G>& L, uint32_t nfl, uint32_t lo_c, uint32_t hi_c, uint32_t wl_r,
+                                  uint32_t wh_r, ChunkOf chunk_of, uint32_t& edge) {
+  // the rows' classes first, all reads issued at once (one LDS round trip:
+  // rows of whole-frame payload, the large-frame case, cost nothing more)
+  uint32_t need = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < NK; k++) {
+    uint32_t a = 0, r = 0;
+    bool ok = false;
+    chunk_of(k, a, r, ok);
+    const uint32_t info = __builtin_amdgcn_readfirstlane(L.rt[r].x);
+    if (ok && !(info & (ROW_FAST | ROW_SKIP))) need |= 1u << k;
+  }
+  uint32_t put = 0;
+#pragma nounroll
+  while (need) {
+    const uint32_t k = __builtin_ctz(need);
+    need &= need - 1;
+    uint32_t a = 0, r = 0;
+    bool ok = false;
+    chunk_of(k, a, r, ok);
+    if (!(a >= lo_c && a < hi_c && a + 16 > wl_r && a < wh_r)) continue;
+    if (!(a >= wl_r && a + 16 <= wh_r)) {
+      edge |= 1u << k;
+      continue;
+    }
+    uint32_t g = L.rt[r].x;
+    uint32_t ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
+    while (ns <= a) {
+      g++;
+      ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
+    }
+    const u32x4 m = chunk_xor(L, nfl, g, a);
+    if (m.x | m.y | m.z | m.w) {
+      u32x4* c = reinterpret_cast<u32x4*>(&L.seg[a]);
+      *c = *c ^ m;
+      put |= 1u << k;
+    }
+  }
+  return put;
+}
+
 // Wait until run j's entry granule, claimed in this call, is published (lane
 // 0); false when the bounded wait timed out (reported). The claimer is run j's
 // own running workgroup, which computes its prologue without waiting for
@@ -1298,7 +1440,7 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
       // the dense pass where the previous pass found many frames and no limit
       // lies in this segment (the serial chase below otherwise, or after it)
       bool dense = false;
-      if (lo_c == 0 && keep == 0 && L.dense >= 2 * G::NSB) {
+      if (lo_c == 0 && keep == 0 && L.dense >= 2 * G::NSB && !L.sgood) {
         const cstate S0 = L.S;
         const bool kn = L.known != 0, pst = L.past != 0;
         const uint64_t se14 = ss + G::SEG + XYWS_MAX_FRAME_HEADER_SIZE;
@@ -1316,7 +1458,15 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
         // at the barrier with their prefetch in flight: work here is hidden,
         // work in the store loop below is not)
         const uint64_t t_r0 = st_on ? __builtin_amdgcn_s_memtime() : 0;
-        if (tid == 0 && !dense) chase_pass(P, L, ss, lo_c, keep);
+        // the stride pass first (exact; regular frames), then lane 0's chase
+        uint32_t k0 = keep;
+        if (!dense && lo_c == 0 && keep == 0) {
+          k0 = stride_pass<G>(P, L, ss, tid);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (tid == 0 && !dense) chase_pass(P, L, ss, lo_c, k0);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1346,6 +1496,14 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
       // this unrolled loop: the next segment's loads are in flight).
       uint32_t edge = 0;
       const uint32_t wave = tid >> 6;
+      const uint32_t put = boundary_chunks<G, G::CH>(
+          L, nfl, lo_c, hi_c, wl_r, wh_r,
+          [&](uint32_t k, uint32_t& a, uint32_t& r, bool& ok) {
+            a = (k * G::NT + tid) * 16u;
+            r = k * (G::NT / 64) + wave;
+            ok = true;
+          },
+          edge);
       u32x4 dprev = {0u, 0u, 0u, 0u};
       // software pipeline: chunk k+1's row word and bytes are read from LDS
       // before chunk k's store
@@ -1371,30 +1529,10 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
           m = u32x4{0u, 0u, 0u, 0u};
           off = OOB;
         } else {
-          const bool in = a >= lo_c && a < hi_c && a + 16 > wl_r && a < wh_r;
+          // (XORed in LDS already when bit k of put is set: boundary_chunks)
           m = u32x4{0u, 0u, 0u, 0u};
-          off = OOB;
-          if (in) {
-            uint32_t g = info;
-            fent e = L.fl[g];
-            uint32_t ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
-            while (ns <= a) {
-              g++;
-              e = L.fl[g];
-              ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
-            }
-            const bool simple = e.ps <= a && e.end >= a + 16 && ns >= a + 16;
-            const bool full = a >= wl_r && a + 16 <= wh_r;
-            if (simple && full) {
-              m = u32x4{e.kw, e.kw, e.kw, e.kw};
-              off = e.kw ? tid * 16u : OOB;
-            } else {
-              off = OOB;
-              edge |= 1u << k;
-            }
-          } else {
-            off = OOB;
-          }
+          off = ((put >> k) & 1u) ? tid * 16u : OOB;
+          (void)a;
         }
         const u32x4 d = v ^ m;
         __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, k * G::NT * 16u, AUX_ST);
@@ -1966,6 +2104,7 @@ XYWS_DEV void decode_range(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint
   if (tid == 0) {
     L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.tmo = 0; L.first_after = NONE;
     L.known = 0;
+    L.sgood = 1;
     L.rng_end = rng_end;
     L.victim = victim ? 1u : 0u;
     L.hn = NONE; L.Wn = NONE; L.succ = P.nflat;
@@ -2069,7 +2208,7 @@ XYWS_DEV uint32_t steal_piece(const run_params& P, lds_t<G>& L, uint32_t tid) {
 // pieces of slower runs (steal_piece) until none is worth taking; the run /
 // piece loop keeps one copy of the prologue and of the chain in the kernel.
 template <class G>
-__device__ __attribute__((noinline)) void finish_call(run_params P, lds_t<G>& L, uint32_t tid);
+__device__ __attribute__((always_inline)) inline void finish_call(run_params P, lds_t<G>& L, uint32_t tid);
 
 template <class G>
 __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
@@ -2106,17 +2245,19 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_runs(run_params P) {
       if (run == 0) {
         // snapshot of the incoming carry for finish_call / k_stream_emit
         // (the caller's carry may alias the carry out, which finish writes)
-        xyws_carry cz;
-        if (P.cin_user) {
-          cz = *P.cin_user;
-        } else {
-          for (int i = 0; i < 64; i++) reinterpret_cast<uint8_t*>(&cz)[i] = 0;
-        }
+        // (in words, through LDS: no private copy)
+        const xyws_carry* cu = P.cin_user ? P.cin_user : &k_zero_carry;
+        uint64_t cw[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) cw[i] = reinterpret_cast<const uint64_t*>(cu)[i];
         // (sc1 stores: another CU's finish reads them)
-        for (int i = 0; i < 8; i++)
-          st_store(reinterpret_cast<uint64_t*>(P.cin) + i, reinterpret_cast<const uint64_t*>(&cz)[i]);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          reinterpret_cast<uint64_t*>(&L.cinc)[i] = cw[i];
+          st_store(reinterpret_cast<uint64_t*>(P.cin) + i, cw[i]);
+        }
         uint64_t c0;
-        L.S = initial_state(P, &cz, c0);
+        L.S = initial_state(P, &L.cinc, c0);
         L.cnt = c0;
         // dense-pass hint for the first segment, as a prologue sets it: the
         // frame at the first boundary is small (run 0 chased its first
@@ -2251,6 +2392,7 @@ XYWS_DEV void chain_start(lds_t<G>& L, const cstate& S, uint64_t hn, uint64_t Wn
   L.S.st &= ~S_CUT;
   L.hn = hn; L.Wn = Wn; L.succ = succ;
   L.known = 1; L.cnt = 0; L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.dense = 0; L.tmo = 0;
+  L.sgood = 1;
   L.first_after = NONE;
   L.best = 0;
   L.rng_end = NONE;
@@ -2385,10 +2527,11 @@ XYWS_DEV void finish_walk(const run_params& P, lds_t<G>& L, uint32_t tid) {
 // hand-overs) and bad hand-overs are repaired (finish_walk). Then the ticket,
 // the done count and the end-of-call words are reset and the epoch advances,
 // so the next call (or graph replay) starts clean without a memset.
-// (not inlined: the record scan and the repair walk stay out of the decode
-// loop's register allocation)
+// (inlined: as a call it cost ~900 B of private segment per lane for the
+// call frame; inlined the decode loop still spills nothing, checked in the
+// ISA, and the private segment is ~190 B, in the prologue and this path)
 template <class G>
-__device__ __attribute__((noinline)) void finish_call(run_params P, lds_t<G>& L, uint32_t tid) {
+__device__ __attribute__((always_inline)) inline void finish_call(run_params P, lds_t<G>& L, uint32_t tid) {
   uint64_t* hw = reinterpret_cast<uint64_t*>(P.head);
   if (tid == 0) {
     const uint64_t bad = st_load(hw + HW_BAD);
@@ -2776,6 +2919,14 @@ XYWS_DEV void store_pass(const run_params& P, const lds_t<G>& L, uint64_t ss, ui
   const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss);
   uint32_t edge = 0;
   const uint32_t wave = tid >> 6;
+  const uint32_t put = boundary_chunks<G, G::CH>(
+      const_cast<lds_t<G>&>(L), nfl, lo_c, hi_c, wl_r, wh_r,
+      [&](uint32_t k, uint32_t& a, uint32_t& r, bool& ok) {
+        a = (k * G::NT + tid) * 16u;
+        r = k * (G::NT / 64) + wave;
+        ok = true;
+      },
+      edge);
   u32x4 dprev = {0u, 0u, 0u, 0u};
   uint2 rw_n = L.rt[wave];
   u32x4 v_n = *reinterpret_cast<const u32x4*>(&L.seg[tid * 16u]);
@@ -2799,27 +2950,9 @@ XYWS_DEV void store_pass(const run_params& P, const lds_t<G>& L, uint64_t ss, ui
       m = u32x4{0u, 0u, 0u, 0u};
       off = OOB;
     } else {
-      const bool in = a >= lo_c && a < hi_c && a + 16 > wl_r && a < wh_r;
       m = u32x4{0u, 0u, 0u, 0u};
-      off = OOB;
-      if (in) {
-        uint32_t g = info;
-        fent e = L.fl[g];
-        uint32_t ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
-        while (ns <= a) {
-          g++;
-          e = L.fl[g];
-          ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
-        }
-        const bool simple = e.ps <= a && e.end >= a + 16 && ns >= a + 16;
-        const bool full = a >= wl_r && a + 16 <= wh_r;
-        if (simple && full) {
-          m = u32x4{e.kw, e.kw, e.kw, e.kw};
-          off = e.kw ? tid * 16u : OOB;
-        } else {
-          edge |= 1u << k;
-        }
-      }
+      off = ((put >> k) & 1u) ? tid * 16u : OOB;  // (boundary_chunks)
+      (void)a;
     }
     const u32x4 d = v ^ m;
     __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, k * G::NT * 16u, AUX_ST);
@@ -2925,6 +3058,14 @@ XYWS_DEV void store_rows(const run_params& P, const lds_t<G>& L, uint64_t ss, ui
   if (CHK && !IO::data_wave(wave)) return;
   const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss);
   uint32_t edge = 0;
+  const uint32_t put = boundary_chunks<G, IO::K>(
+      const_cast<lds_t<G>&>(L), nfl, 0u, hi_c, wl_r, wh_r,
+      [&](uint32_t k, uint32_t& a, uint32_t& r, bool& ok) {
+        ok = IO::valid(wave, k);
+        r = ok ? IO::row(wave, k) : 0u;
+        a = r * 1024u + lane * 16u;
+      },
+      edge);
   u32x4 dprev = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (uint32_t k = 0; k < IO::K; k++) {
@@ -2945,32 +3086,10 @@ XYWS_DEV void store_rows(const run_params& P, const lds_t<G>& L, uint64_t ss, ui
       m = u32x4{0u, 0u, 0u, 0u};
       off = OOB;
     } else {
-      const bool in = a < hi_c && a + 16 > wl_r && a < wh_r;
       m = u32x4{0u, 0u, 0u, 0u};
-      off = OOB;
-      if (in) {
-        uint32_t g = info;
-        fent e = L.fl[g];
-        uint32_t ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
-        while (ns <= a) {
-          g++;
-          e = L.fl[g];
-          ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
-        }
-        const bool simple = e.ps <= a && e.end >= a + 16 && ns >= a + 16;
-        const bool full = a >= wl_r && a + 16 <= wh_r;
-        if (simple && full) {
-          m = u32x4{e.kw, e.kw, e.kw, e.kw};
-          off = e.kw ? lane * 16u : OOB;
-        } else {
-          edge |= 1u << k;
-        }
-      }
+      off = ((put >> k) & 1u) ? lane * 16u : OOB;  // (boundary_chunks)
     }
-    if (!ok) {
-      off = OOB;
-      edge &= ~(1u << k);
-    }
+    if (!ok) off = OOB;
     const u32x4 d = v ^ m;
     __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, r * 1024u, AUX_ST);
     // (see run_chain: the store's data registers stay live past the next store)
