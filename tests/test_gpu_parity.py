@@ -205,6 +205,67 @@ def test_dense_frames_with_header_like_payloads(ws, oracle, fake):
     assert carry_list(dec.carry()) == carry_list(carry)
 
 
+@pytest.mark.parametrize("mode", ["fused", "runs1k", "runs1k_giveup"])
+@pytest.mark.parametrize("kind", ["stride_fakes", "size_changes", "long_lengths", "segment_ends"])
+def test_stride_pass_adversarial(ws, oracle, mode, kind):
+    """The run decoder's stride pass (lane i parses the header at X + i*F,
+    one ballot accepts frames up to the first size change) on streams made
+    to mislead it: runs of equal frames whose payloads hold valid headers of
+    the same size at every stride offset from the payload start (a stride
+    taken from the wrong origin would accept them), runs whose size changes
+    every few frames, 126/127-form lengths and 2^31+ lengths in a run,
+    and runs crossing segment ends / the batch end. GPU vs oracle: bytes,
+    count, descriptors, carry."""
+    rng = streams.SplitMix(0x57D1 + len(kind))
+    out = bytearray()
+    target = 3 << 20 if mode == "fused" else 200000
+    while len(out) < target:
+        if kind == "stride_fakes":
+            plen = 100 + rng.below(300)
+            # the payload: valid headers of frames of exactly `size` bytes at every
+            # offset d, d + size, ... from a random d (fake starts on a shifted lattice)
+            fake = streams.header(0x82, plen, rng.bytes(4), None)
+            size = len(fake) + plen
+            d = 1 + rng.below(size - 1)
+            body = bytearray(rng.bytes(plen))
+            for o in range(d % size, plen - len(fake), size):
+                body[o:o + len(fake)] = fake
+            for _ in range(1 + rng.below(40)):
+                out += streams.header(0x82, plen, rng.bytes(4), None) + bytes(body)
+        elif kind == "size_changes":
+            plen = rng.below(600)
+            for _ in range(1 + rng.below(6)):
+                out += streams.frame(rng, 0x82, plen)
+        elif kind == "long_lengths":
+            for _ in range(1 + rng.below(20)):
+                out += streams.frame(rng, 0x81, 126 + rng.below(2))  # 126 form at the 7-bit edge
+            out += streams.frame(rng, 0x82, 65536 + rng.below(3))    # 127 form
+            if rng.below(8) == 0:
+                out += streams.header(0x82, (1 << 31) + rng.below(5), rng.bytes(4), None)  # runs past the end
+                break
+        else:  # equal frames whose headers straddle 1 KiB and 128 KiB boundaries
+            plen = 1024 - 8 - rng.below(24)
+            for _ in range(1 + rng.below(200)):
+                out += streams.frame(rng, 0x82, plen)
+    src = bytes(out)
+    for cut in (len(src), len(src) - 5, len(src) - 1000):
+        piece = src[:cut]
+        view, _ = dev_bytes(piece)
+        dec = ws.frame_decoder(**MODES[mode])
+        ob = np.frombuffer(piece, np.uint8).copy()
+        ofr, carry, on = oracle.decode_stream(ob, cap=len(piece) // 2 + 2)
+        r = dec.decode(view, cap=on + 2)
+        assert r.nframes == on, (kind, mode, cut)
+        assert host(view) == ob.tobytes(), (kind, mode, cut)
+        assert frames_list(r.frames(), True) == frames_list(ofr, True)
+        assert carry_list(dec.carry()) == carry_list(carry)
+        # and without descriptors (the path the bench times; the decoder choice)
+        view2, _ = dev_bytes(piece)
+        dec2 = ws.frame_decoder(**MODES[mode])
+        r2 = dec2.decode(view2, cap=0)
+        assert r2.nframes == on and host(view2) == ob.tobytes()
+
+
 # --------------------------------------------------------------------------- indexed
 def test_indexed_matches_golden(ws):
     g = load_golden("streams.json")["cases"]["lengths"]

@@ -813,12 +813,13 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
 
 // Stride pass (wave 0, every lane; the first pass of a segment, before lane
 // 0's serial chase). In a stream of equal frames the frame after X starts at
-// X + F, F the size of the frame that ends at X; lane i parses the header at
-// X + i*F from LDS (the serial chase's 32-bit parse, below the same stop).
-// Lane 0's position is exact (X); lane i's is exact when lanes 0..i-1 each
-// found a frame of exactly F bytes (induction from X), so ONE ballot accepts
-// lanes 0..m, m the first lane whose frame is not F bytes long (its start is
-// exact too; its own size ends the step). A step decides up to 64 frames in
+// X + F, F the size of the frame that ends at X; lane i parses the headers at
+// X + i*F and X + (64 + i)*F from LDS (the serial chase's 32-bit parse,
+// below the same stop). Position 0 is exact (X); position i is exact when
+// positions 0..i-1 each hold a frame of exactly F bytes (induction from X),
+// so ONE ballot accepts positions 0..m, m the first whose frame is not F
+// bytes long (its start is exact too; its own size ends the step). A step
+// decides up to 128 frames in
 // one LDS round trip where the serial chase takes one hop per frame, and it
 // is exact whatever the bytes: no accepted position is a guess. Steps repeat
 // from the new X while one accepts STRIDE_MIN frames or more. Returns the
@@ -852,26 +853,40 @@ XYWS_DEV uint32_t stride_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uin
   uint32_t n = n0, total = 0, x = (uint32_t)(S0.X - ss), f = (uint32_t)F;
   cstate S = S0;
   for (;;) {
-    const uint64_t p64 = (uint64_t)x + (uint64_t)lane * f;
-    const bool valid = p64 < st && n + lane < G::FCAP;
-    const uint32_t p = (uint32_t)p64;
-    uint32_t hl = 0, plen = 0, key = 0, b01 = 0;
-    bool ok = false;
-    if (valid) ok = parse_rel<G>(L, p, hl, plen, key, b01);
-    const uint64_t vm = __ballot(valid), okm = __ballot(ok), mm = __ballot(ok && hl + plen == f);
-    const uint32_t m = mm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~mm);  // first lane without a match
-    uint32_t a = (m < 64 && ((okm >> m) & 1ull)) ? m + 1 : m;
-    const uint32_t nv = (uint32_t)__builtin_popcountll(vm);  // (valid lanes are 0..nv-1)
+    // two positions per lane: frames x + lane*f (A) and x + (64 + lane)*f (B)
+    const uint64_t pa64 = (uint64_t)x + (uint64_t)lane * f, pb64 = pa64 + 64ull * f;
+    const bool va = pa64 < st && n + lane < G::FCAP, vb = pb64 < st && n + 64 + lane < G::FCAP;
+    const uint32_t pa = (uint32_t)pa64, pb = (uint32_t)pb64;
+    uint32_t hla = 0, pla = 0, kya = 0, hlb = 0, plb = 0, kyb = 0, b01 = 0;
+    bool oka = false, okb = false;
+    if (va) oka = parse_rel<G>(L, pa, hla, pla, kya, b01);
+    if (vb) okb = parse_rel<G>(L, pb, hlb, plb, kyb, b01);
+    const uint64_t vma = __ballot(va), vmb = __ballot(vb);
+    const uint64_t oma = __ballot(oka), omb = __ballot(okb);
+    const uint64_t mma = __ballot(oka && hla + pla == f), mmb = __ballot(okb && hlb + plb == f);
+    // the first position without a match, in the sequence A then B
+    const uint32_t m = mma != ~0ull ? (uint32_t)__builtin_ctzll(~mma)
+                                    : 64u + (mmb == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~mmb));
+    const bool okm = m < 64 ? ((oma >> m) & 1ull) != 0 : (m < 128 && ((omb >> (m - 64)) & 1ull) != 0);
+    uint32_t a = okm ? m + 1 : m;  // (the first mismatch's start is exact: its own size ends the step)
+    const uint32_t nv = (uint32_t)__builtin_popcountll(vma) + (uint32_t)__builtin_popcountll(vmb);
     if (a > nv) a = nv;
     if (a == 0) break;
     if (lane < a) {
-      const uint32_t ps = p + hl;
-      L.fl[n + lane] = fent{p, ps, ps + plen, rotr8(key, 0u - ps)};
+      const uint32_t ps = pa + hla;
+      L.fl[n + lane] = fent{pa, ps, ps + pla, rotr8(kya, 0u - ps)};
+    }
+    if (64 + lane < a) {
+      const uint32_t ps = pb + hlb;
+      L.fl[n + 64 + lane] = fent{pb, ps, ps + plb, rotr8(kyb, 0u - ps)};
     }
     // the last accepted frame is the chain state
-    const uint32_t l = a - 1;
-    const uint32_t lp = __builtin_amdgcn_readlane(p, l), lhl = __builtin_amdgcn_readlane(hl, l);
-    const uint32_t lpl = __builtin_amdgcn_readlane(plen, l), lkey = __builtin_amdgcn_readlane(key, l);
+    const uint32_t l = a - 1, ll = l & 63u;
+    const bool inb = l >= 64;
+    const uint32_t lp = __builtin_amdgcn_readlane(inb ? pb : pa, ll);
+    const uint32_t lhl = __builtin_amdgcn_readlane(inb ? hlb : hla, ll);
+    const uint32_t lpl = __builtin_amdgcn_readlane(inb ? plb : pla, ll);
+    const uint32_t lkey = __builtin_amdgcn_readlane(inb ? kyb : kya, ll);
     S.cov_start = ss + lp;
     S.cov_ps = ss + lp + lhl;
     S.X = ss + lp + lhl + lpl;
