@@ -17,21 +17,25 @@ import sys
 
 def per_launch(d, counter, kernel=None):
     """Average counter value per launch of `kernel` (a name substring); by
-    default the decoder kernel (k_stream_runs / k_stream_sweep) with the most
-    launches in the pass, i.e. the one the timed steps ran (the decoder
-    choice may serve the first warm-up call with the other one)."""
-    vals = {}
+    default the decoder kernel (k_stream_runs / k_stream_sweep) of the last
+    dispatch, i.e. the one the timed steps ran (the decoder choice serves the
+    first calls, before the first one has finished, with the run decoder)."""
+    vals, last = {}, None
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
+        rows = list(csv.DictReader(open(f)))
+        if rows and "Dispatch_Id" in rows[0]:
+            rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        for r in rows:
             name = r["Kernel_Name"]
             hit = (kernel in name) if kernel else ("k_stream_runs" in name or "k_stream_sweep" in name)
             if hit and r["Counter_Name"] == counter:
                 k = "k_stream_sweep" if "k_stream_sweep" in name else ("k_stream_runs" if "k_stream_runs" in name
                                                                         else kernel)
                 vals.setdefault(k, []).append(float(r["Counter_Value"]))
+                last = k
     if not vals:
         raise SystemExit(f"no {counter} rows for {kernel or 'the decoder kernels'} under {d}")
-    k = max(vals, key=lambda x: len(vals[x]))
+    k = last  # (the timed steps are the last dispatches)
     v = vals[k]
     return sum(v) / len(v), len(v), k
 
@@ -60,7 +64,7 @@ def main():
         "hbm_write_bytes_per_launch": int(wk * 1024),
         "hbm_bytes_per_launch": int(fk * 2 * 1024 + wk * 1024),
         "correction": "FETCH_SIZE x2 (gfx950 streaming-read undercount), KiB -> bytes",
-        "src_sha": source_hash(),
+        "src_sha": os.environ.get("PMC_SRC_SHA") or source_hash(),  # (override: the profiled tree's hash)
         "profile": profile,
     }
     data = json.load(open(out)) if os.path.exists(out) else {}
