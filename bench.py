@@ -721,11 +721,15 @@ def main():
             dec.opts &= ~_lib.OPT_STATS
             out = (C.c_uint64 * _lib.NSTATS)()
             dec.ctx.L.xyws_debug_stats(dec.ctx.h, C.c_void_p(stream.cuda_stream), out)
+        if decoder and decoder.startswith("sweep"):  # (the sweep's own timing split: ST_SWT_*, per segment)
+            names[16:26] = ["cyc_claim_wait", "cyc_phase_a", "cyc_phase_b", "cyc_data_barrier", "cyc_data_load",
+                            "cyc_records", "cyc_data_store", "cyc_data_fill", "cyc_iteration", "cyc_predict"]
         st = {k: v for k, v in zip(names, list(out))}
-        nrun = max(1, st["runs"] + 1)
+        nrun = max(1, (st["dense_passes"] if decoder and decoder.startswith("sweep") else st["runs"] + 1))
         for k in list(st):
             if k.startswith("cyc_"):
-                st[k.replace("cyc_", "us_per_run_")] = round(st.pop(k) / nrun / 2100.0, 3)
+                per = "us_per_segment_" if decoder and decoder.startswith("sweep") else "us_per_run_"
+                st[k.replace("cyc_", per)] = round(st.pop(k) / nrun / 2100.0, 3)
         print(json.dumps({"stats": st}), flush=True)
 
     # parity after the timed region: every copy against the reference digest

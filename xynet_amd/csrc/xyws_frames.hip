@@ -31,6 +31,7 @@ constexpr uint32_t FT = 256;           // threads per block, frame-list kernels
 constexpr uint32_t SB = 4 * FT;        // items per scan block (4 per lane)
 constexpr uint32_t GTILE = 16384;      // gather tile (bytes of output)
 constexpr uint32_t GLDS = 512;         // items staged per tile
+constexpr uint32_t GFAST_ITEMS = 3;    // k_gather's fast path: tiles of at most this many items
 constexpr uint64_t U64MAX = ~0ull;
 
 // ---------------------------------------------------------------- header build
@@ -357,6 +358,27 @@ XYWS_DEV u32x4 src16(const gparams& G, int64_t p) {
   return u32x4{w[0], w[1], w[2], w[3]};
 }
 
+// Bytes [sh, sh + 16) of the 32 bytes x | y (sh in [0, 16)).
+XYWS_DEV u32x4 funnel16(const u32x4& x, const u32x4& y, uint32_t sh) {
+  const uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+  const uint32_t d = sh >> 2, b = sh & 3u;
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t lo = v[k], hi = v[k + 1];
+#pragma unroll
+    for (uint32_t s = 1; s < 4; s++)
+      if (d == s) { lo = v[s + k]; hi = v[s + k + 1]; }
+    w[k] = b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
+  }
+  return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+XYWS_DEV u32x4 shfl_down16(const u32x4& x) {
+  return u32x4{(uint32_t)__shfl_down((int)x.x, 1, 64), (uint32_t)__shfl_down((int)x.y, 1, 64),
+               (uint32_t)__shfl_down((int)x.z, 1, 64), (uint32_t)__shfl_down((int)x.w, 1, 64)};
+}
+
 // Items staged per tile (struct of arrays in LDS).
 struct gstage {
   uint64_t dst[GLDS + 1];  // output start (q coordinate); dst[k] of the item after the last: its start
@@ -372,7 +394,11 @@ struct gstage {
 // header words, payload bytes from two aligned 16-byte source loads and a
 // funnel shift, XORed with the rotated key word, each selected by its byte
 // mask. One 16-byte store per chunk (byte stores only at the output's ends).
-// Tiles with more items than fit in LDS take the per-byte path.
+// Chunks inside one item's payload (all of them for large frames) take a fast
+// path first: the lane's four source lines are loaded at once, and the second
+// line a misaligned chunk needs is the next lane's first (a lane shuffle), so
+// every source line is read once. Tiles with more items than fit in LDS take
+// the per-byte path.
 __global__ void __launch_bounds__(FT) k_gather(gparams G, const uint64_t* __restrict__ map, uint64_t ntiles) {
   __shared__ gstage S;
   __shared__ uint64_t s_f0, s_f1;
@@ -406,10 +432,68 @@ __global__ void __launch_bounds__(FT) k_gather(gparams G, const uint64_t* __rest
       if (threadIdx.x == 0) S.dst[f1 - f0] = G.off[f1];
     }
     __syncthreads();
+    constexpr uint32_t GC = GTILE / 16 / FT;
+    uint32_t fastm = 0;  // chunks done by the fast path
+    // (tiles of a few large items: with many small ones most waves hold a
+    // boundary chunk in every round, and the per-chunk loop below is the whole
+    // cost: the fast path's own round trip would only add to it)
+    if (in_lds && f1 - f0 <= GFAST_ITEMS) {
+      const uint32_t n = (uint32_t)(f1 - f0), lane = __lane_id();
+      // two chunks per round (registers: the per-chunk loop below runs in the
+      // same kernel at the occupancy this path leaves)
+      constexpr uint32_t GH = 2;
+#pragma unroll 1
+      for (uint32_t c0 = 0; c0 < GC; c0 += GH) {
+      u32x4 x[GH], y[GH];
+      uint32_t sh[GH], kw[GH], nbm = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < GH; j++) {
+        const uint32_t c = c0 + j;
+        const uint64_t a = t0 + (uint64_t)(c * FT + threadIdx.x) * 16;
+        const int64_t ca = (int64_t)a - (int64_t)o0;
+        const uint64_t qa = a > o0 ? a - o0 : 0;
+        uint32_t g = 0, hi = n;
+        while (hi - g > 1) {
+          const uint32_t m = (g + hi) >> 1;
+          if (S.dst[m] <= qa) g = m; else hi = m;
+        }
+        const int64_t ds = (int64_t)S.dst[g], de = (int64_t)S.dst[g + 1], ps = ds + S.h[g];
+        const int64_t sp = (int64_t)S.soff[g] + (ca - ps);  // source payload index of chunk byte 0
+        const bool simple = a >= o0 && a + 16 <= o1 && ps <= ca && de >= ca + 16 && sp + 16 <= (int64_t)G.src_len;
+        x[j] = y[j] = u32x4{0u, 0u, 0u, 0u};
+        sh[j] = 0;
+        kw[j] = 0;
+        if (simple) {
+          const uint64_t A = G.src_lo + (uint64_t)sp, la = A & ~15ull;
+          sh[j] = (uint32_t)(A & 15u);
+          kw[j] = rotr8(S.key[g], (uint32_t)(ca - ps));
+          x[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(G.src + la));
+          fastm |= 1u << c;
+          // the second line: the next lane's first when its chunk is the same
+          // item's next 16 bytes (its line la + 16), else loaded here
+          const bool nb = lane < 63 && de >= ca + 32 && a + 32 <= o1 && sp + 32 <= (int64_t)G.src_len;
+          if (sh[j] && !nb) y[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(G.src + la + 16));
+          if (nb) nbm |= 1u << j;
+        }
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < GH; j++) {
+        const uint32_t c = c0 + j;
+        const u32x4 yn = shfl_down16(x[j]);
+        if (((fastm >> c) & 1u) && sh[j]) {
+          x[j] = funnel16(x[j], ((nbm >> j) & 1u) ? yn : y[j], sh[j]);
+        }
+        if ((fastm >> c) & 1u) {
+          const uint64_t a = t0 + (uint64_t)(c * FT + threadIdx.x) * 16;
+          __builtin_nontemporal_store(x[j] ^ u32x4{kw[j], kw[j], kw[j], kw[j]}, reinterpret_cast<u32x4*>(G.out + a));
+        }
+      }
+      }
+    }
 #pragma unroll 1
     for (uint32_t c = 0; c < GTILE / 16 / FT; c++) {
       const uint64_t a = t0 + (uint64_t)(c * FT + threadIdx.x) * 16;  // aligned out[] position
-      if (a + 16 <= o0 || a >= o1) continue;
+      if (a + 16 <= o0 || a >= o1 || ((fastm >> c) & 1u)) continue;
       const uint64_t qa = a > o0 ? a - o0 : 0;  // first output byte of the chunk
       if (!in_lds) {
         // many tiny items: byte by byte from memory
@@ -639,60 +723,174 @@ __global__ void __launch_bounds__(FT) k_rs_msgs(const uint64_t* dev_n, uint64_t 
 // lane per 16-byte chunk, neighbours read for sequences crossing chunks.
 XYWS_DEV uint32_t lead_len(uint32_t c) { return c >= 0xF0u ? 4u : c >= 0xE0u ? 3u : c >= 0xC0u ? 2u : 0u; }
 
+// UTF-8 tiles: UT bytes of out[] per tile; map[t] = the message holding the
+// tile's first byte (one lane per message marks its tiles, as k_tile_map
+// does for the gather), so a tile finds its messages with two loads and skips
+// at once when none of them is a text message.
+constexpr uint32_t UT = 65536;
+__global__ void __launch_bounds__(FT) k_utf8_map(const uint64_t* nmsg_p, const xyws_message* msgs,
+                                                 uint64_t msg_cap, uint64_t out_lo, uint64_t out_cap,
+                                                 uint64_t* map, uint64_t ntiles) {
+  const uint64_t m = (uint64_t)blockIdx.x * FT + threadIdx.x;
+  const uint64_t nm0 = *nmsg_p, nm = nm0 < msg_cap ? nm0 : msg_cap;
+  if (m >= nm) return;
+  const uint64_t qs = msgs[m].out_off, qe0 = qs + msgs[m].length, qe = qe0 < out_cap ? qe0 : out_cap;
+  if (qs >= qe) return;
+  if (qs == 0) map[0] = m;
+  uint64_t t = (qs + out_lo + UT - 1) / UT;
+  if (t == 0) t = 1;
+  const uint64_t t1 = (qe + out_lo + UT - 1) / UT;
+  for (; t < t1 && t < ntiles; t++) map[t] = m;
+}
+
+// The tile's messages (up to UMS) are staged in LDS with a bad flag each; a
+// lane marks its message's flag, and the flags reach the records once per tile
+// (one atomic per bad message per tile, not one per byte or chunk).
+constexpr uint32_t UMS = 512;
+struct ustage {
+  uint64_t mo[UMS], me[UMS];
+  uint32_t ty[UMS];  // status bits | text (bit 31)
+  uint32_t bad[UMS];
+};
+constexpr uint32_t UTEXT = 1u << 31;
+
 __global__ void __launch_bounds__(FT) k_utf8(const uint8_t* out, uint64_t out_lo, uint64_t out_cap,
-                                             const uint64_t* nmsg_p, xyws_message* msgs, uint64_t msg_cap) {
+                                             const uint64_t* nmsg_p, xyws_message* msgs, uint64_t msg_cap,
+                                             const uint64_t* map, uint64_t ntiles) {
+  __shared__ ustage U;
+  __shared__ uint32_t s_text;
+  __shared__ uint64_t s_m0, s_m1;
   const uint64_t nm0 = *nmsg_p, nm = nm0 < msg_cap ? nm0 : msg_cap;
   if (!nm) return;
   const uint64_t total0 = msgs[nm - 1].out_off + msgs[nm - 1].length;
   const uint64_t total = total0 < out_cap ? total0 : out_cap;
-  const uint64_t nch = (total + 15) / 16;
-  for (uint64_t ch = (uint64_t)blockIdx.x * FT + threadIdx.x; ch < nch; ch += (uint64_t)gridDim.x * FT) {
-    const uint64_t q0 = ch * 16;
-    // the last message starting at or before q0
-    uint64_t lo = 0, hi = nm;
-    while (hi - lo > 1) {
-      const uint64_t md = (lo + hi) >> 1;
-      if (msgs[md].out_off <= q0) lo = md; else hi = md;
+  if (!total) return;
+  const uint64_t nt = (out_lo + total + UT - 1) / UT;
+  for (uint64_t tile = blockIdx.x; tile < nt && tile < ntiles; tile += gridDim.x) {
+    if (threadIdx.x == 0) {
+      s_m0 = map[tile];
+      s_m1 = tile + 1 < nt ? map[tile + 1] : nm - 1;  // (inclusive)
+      s_text = 0;
     }
-    uint64_t m = lo;
-    for (uint32_t t = 0; t < 16; t++) {
-      const uint64_t q = q0 + t;
-      if (q >= total) break;
-      while (m + 1 < nm && msgs[m + 1].out_off <= q) m++;
-      const uint64_t mo = msgs[m].out_off, me = mo + msgs[m].length;
-      if (msgs[m].opcode != XYWS_FLAG_OP_TEXT || q < mo || q >= me) continue;
-      const uint32_t mst = msgs[m].status;
-      const uint32_t c = out[out_lo + q];
-      bool bad = false;
-      if (c < 0x80u) {
-      } else if (c < 0xC0u) {
-        // a continuation byte: a lead within 3 bytes before must claim it
-        bool claimed = false;
-        for (uint32_t d = 1; d <= 3 && !claimed; d++) {
-          if (q < mo + d) break;
-          if (lead_len(out[out_lo + q - d]) > d) claimed = true;
-        }
-        bad = !claimed;
-      } else if (c == 0xC0u || c == 0xC1u || c >= 0xF5u) {
-        bad = true;
-      } else {
-        const uint32_t L = lead_len(c);
-        if (q + L > me || q + L > total) {
-          // cut by the end: invalid only in a complete message whose bytes
-          // all fit (an incomplete message continues in a later batch)
-          bad = (mst & XYWS_MSG_COMPLETE) && !(mst & XYWS_MSG_TRUNCATED);
-        } else {
-          for (uint32_t d = 1; d < L; d++)
-            if ((out[out_lo + q + d] & 0xC0u) != 0x80u) bad = true;
-          const uint32_t c1 = out[out_lo + q + 1];
-          if (c == 0xE0u && c1 < 0xA0u) bad = true;  // overlong
-          if (c == 0xEDu && c1 > 0x9Fu) bad = true;  // surrogates
-          if (c == 0xF0u && c1 < 0x90u) bad = true;  // overlong
-          if (c == 0xF4u && c1 > 0x8Fu) bad = true;  // above U+10FFFF
-        }
+    __syncthreads();
+    const uint64_t m0 = s_m0, m1 = s_m1 < nm ? s_m1 : nm - 1;
+    const bool inl = m1 - m0 < UMS;  // the tile's messages staged in LDS
+    for (uint64_t m = m0 + threadIdx.x; m <= m1; m += FT) {
+      const xyws_message r = msgs[m];
+      const bool text = r.opcode == XYWS_FLAG_OP_TEXT && r.length;
+      if (text) s_text = 1;
+      if (inl) {
+        const uint32_t k = (uint32_t)(m - m0);
+        U.mo[k] = r.out_off;
+        U.me[k] = r.out_off + r.length;
+        U.ty[k] = r.status | (r.opcode == XYWS_FLAG_OP_TEXT ? UTEXT : 0u);
+        U.bad[k] = 0;
       }
-      if (bad) atomicOr(&msgs[m].status, XYWS_MSG_UTF8_BAD);
     }
+    __syncthreads();
+    // message m's fields, from LDS or the records
+    auto mo_of = [&](uint64_t m) -> uint64_t { return inl ? U.mo[m - m0] : msgs[m].out_off; };
+    auto me_of = [&](uint64_t m) -> uint64_t { return inl ? U.me[m - m0] : msgs[m].out_off + msgs[m].length; };
+    auto ty_of = [&](uint64_t m) -> uint32_t {
+      return inl ? U.ty[m - m0] | (U.bad[m - m0] ? XYWS_MSG_UTF8_BAD : 0u)
+                 : msgs[m].status | (msgs[m].opcode == XYWS_FLAG_OP_TEXT ? UTEXT : 0u);
+    };
+    auto mark = [&](uint64_t m, uint32_t ty) {
+      if (ty & XYWS_MSG_UTF8_BAD) return;
+      if (inl) U.bad[m - m0] = 1;
+      else atomicOr(&msgs[m].status, XYWS_MSG_UTF8_BAD);
+    };
+    if (s_text) {
+      // the tile's 16-byte chunks in out[] coordinates q = position - out_lo
+      const uint64_t t0 = tile * UT;
+      for (uint32_t c = threadIdx.x; c < UT / 16; c += FT) {
+        const uint64_t a = t0 + (uint64_t)c * 16;  // out[] byte position
+        if (a + 16 <= out_lo) continue;
+        const uint64_t q0 = a > out_lo ? a - out_lo : 0;
+        if (q0 >= total) break;
+        // the chunk's bytes: one 16-byte load when it lies inside the written
+        // range, else byte loads of the bytes that do (the rest read as 0)
+        uint32_t w[4];
+        if (a >= out_lo && a + 16 <= out_lo + total && !((uintptr_t)out & 15u)) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(out + a);
+          w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else {
+          w[0] = w[1] = w[2] = w[3] = 0;
+          for (uint32_t t = 0; t < 16; t++)
+            if (a + t >= out_lo && a + t < out_lo + total) w[t >> 2] |= (uint32_t)out[a + t] << (8u * (t & 3u));
+        }
+        // ASCII bytes are valid anywhere, and a lead byte before the chunk
+        // checks its own continuations: an all-ASCII chunk has nothing to do
+        if (!((w[0] | w[1] | w[2] | w[3]) & 0x80808080u)) continue;
+        // the last message starting at or before q0, among [m0, m1]
+        uint64_t lo = m0, hi = m1 + 1;
+        while (hi - lo > 1) {
+          const uint64_t md = (lo + hi) >> 1;
+          if (mo_of(md) <= q0) lo = md; else hi = md;
+        }
+        uint64_t m = lo;
+        uint64_t mo = mo_of(m), me = me_of(m);
+        uint64_t nx = m + 1 <= m1 ? mo_of(m + 1) : ~0ull;
+        uint32_t ty = ty_of(m);
+        bool bad = false;  // for message m, reported once when m changes
+        for (uint32_t t = 0; t < 16; t++) {
+          const uint64_t pq = a + t;
+          if (pq < out_lo) continue;
+          const uint64_t q = pq - out_lo;
+          if (q >= total) break;
+          if (nx <= q) {
+            if (bad) mark(m, ty);
+            bad = false;
+            while (m + 1 <= m1 && mo_of(m + 1) <= q) m++;
+            mo = mo_of(m);
+            me = me_of(m);
+            nx = m + 1 <= m1 ? mo_of(m + 1) : ~0ull;
+            ty = ty_of(m);
+          }
+          if (!(ty & UTEXT) || q < mo || q >= me || bad || (ty & XYWS_MSG_UTF8_BAD)) continue;
+          const uint32_t ch = (w[t >> 2] >> (8u * (t & 3u))) & 0xFFu;
+          if (ch < 0x80u) {
+          } else if (ch < 0xC0u) {
+            // a continuation byte: a lead within 3 bytes before must claim it
+            bool claimed = false;
+            for (uint32_t d = 1; d <= 3 && !claimed; d++) {
+              if (q < mo + d) break;
+              const uint32_t pb = t >= d ? (w[(t - d) >> 2] >> (8u * ((t - d) & 3u))) & 0xFFu
+                                         : out[out_lo + q - d];
+              if (lead_len(pb) > d) claimed = true;
+            }
+            bad = !claimed;
+          } else if (ch == 0xC0u || ch == 0xC1u || ch >= 0xF5u) {
+            bad = true;
+          } else {
+            const uint32_t L = lead_len(ch);
+            if (q + L > me || q + L > total) {
+              // cut by the end: invalid only in a complete message whose bytes
+              // all fit (an incomplete message continues in a later batch)
+              bad = (ty & XYWS_MSG_COMPLETE) && !(ty & XYWS_MSG_TRUNCATED);
+            } else {
+              uint32_t c1 = 0;
+              for (uint32_t d = 1; d < L; d++) {
+                const uint32_t cb = t + d < 16 ? (w[(t + d) >> 2] >> (8u * ((t + d) & 3u))) & 0xFFu
+                                               : out[out_lo + q + d];
+                if ((cb & 0xC0u) != 0x80u) bad = true;
+                if (d == 1) c1 = cb;
+              }
+              if (ch == 0xE0u && c1 < 0xA0u) bad = true;  // overlong
+              if (ch == 0xEDu && c1 > 0x9Fu) bad = true;  // surrogates
+              if (ch == 0xF0u && c1 < 0x90u) bad = true;  // overlong
+              if (ch == 0xF4u && c1 > 0x8Fu) bad = true;  // above U+10FFFF
+            }
+          }
+        }
+        if (bad) mark(m, ty);
+      }
+    }
+    __syncthreads();
+    if (inl)
+      for (uint64_t m = m0 + threadIdx.x; m <= m1; m += FT)
+        if (U.bad[m - m0] && !(U.ty[m - m0] & XYWS_MSG_UTF8_BAD)) atomicOr(&msgs[m].status, XYWS_MSG_UTF8_BAD);
+    __syncthreads();
   }
 }
 
@@ -868,9 +1066,12 @@ int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, const 
     if ((rc = hip_err(hipGetLastError()))) return rc;
   }
   if ((opts & XYWS_REASM_UTF8) && out_cap && msg_cap) {
-    const uint64_t chunks = (out_cap + 15) / 16;
-    hipLaunchKernelGGL(k_utf8, dim3(grid_for(chunks, FT, 4096)), dim3(FT), 0, s, (const uint8_t*)G.out, G.out_lo,
-                       out_cap, (const uint64_t*)(tot + 1), dev_msgs, msg_cap);
+    // (the gather's tile map is done with: the messages' UTF-8 tile map in its place)
+    const uint64_t utiles = (G.out_lo + out_cap + UT - 1) / UT + 1;
+    hipLaunchKernelGGL(k_utf8_map, dim3((msg_cap + FT - 1) / FT), dim3(FT), 0, s, (const uint64_t*)(tot + 1),
+                       (const xyws_message*)dev_msgs, msg_cap, G.out_lo, out_cap, tmap, utiles);
+    hipLaunchKernelGGL(k_utf8, dim3(grid_for(utiles, 1, 4096)), dim3(FT), 0, s, (const uint8_t*)G.out, G.out_lo,
+                       out_cap, (const uint64_t*)(tot + 1), dev_msgs, msg_cap, (const uint64_t*)tmap, utiles);
     if ((rc = hip_err(hipGetLastError()))) return rc;
   }
   return XYWS_OK;

@@ -45,6 +45,7 @@ int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_ru
 #define XYWS_OPT_DIAG 0x80000u     // diagnostics: no prefetch during the prologue scan (timing only)
 #define XYWS_OPT_TEST_GIVEUP 0x100000u // tests: odd runs give up on their successor at once (the path
                                        // of a successor whose workgroup has not started; finish bridges it)
+#define XYWS_OPT_NO_LATTICE 0x200000u   // experiment (run decoder): no lattice passes (row table and walk only)
 #define XYWS_OPT_STEAL 0x400000u       // work stealing between runs (off by default: measured no faster on c1-c4)
 #define XYWS_OPT_TEST_STEAL 0x800000u  // tests: stealing on, every fourth run starts late, pieces of 1 segment and up
 #define XYWS_OPT_SWEEP 0x1000000u      // the sweep decoder (segment claiming) instead of the run decoder;

@@ -303,10 +303,14 @@ struct __attribute__((aligned(16))) lds_t {
   uint4 dlast[G::NSB];
   uint32_t dense;  // frames of the previous pass (the dense pass is tried after a dense one)
   uint32_t sgood;  // the stride pass serves dense segments (cleared when it did not cover one)
+  // lattice pass (run_chain): entries 1.. start at ar_x0 + (i - 1) * ar_f
+  uint32_t ar, ar_x0, ar_f;
   uint32_t nrec;   // descriptors requested: frame starts the current item recorded
   // sweep decoder: claimed segments (current, next, claimed ahead), the spec
-  // entry and state, the entering state from the look-back, decisions
-  uint64_t sw_cur, sw_next, sw_ahead, sw_h, sw_ref, sw_fsz, sw_pcur, sw_fcur, sw_vs;
+  // entry and state, the entering state from the look-back, decisions; the
+  // stride prediction of the current segment (pcur, fcur) and of the next
+  // (pnx, fnx, made when it is known: the top of the segment loop)
+  uint64_t sw_cur, sw_next, sw_ahead, sw_h, sw_ref, sw_fsz, sw_pcur, sw_fcur, sw_pnx, sw_fnx, sw_vs;
   cstate sw_spec, sw_in, sw_vU;
   uint32_t sw_act, sw_single, sw_cnt_spec, sw_fast, sw_padok;
   uint64_t sw_t[9];  // sweep timing split (XYWS_OPT_STATS): see ST_SWT_*
@@ -595,11 +599,10 @@ XYWS_DEV uint32_t range_mask32(uint32_t a, uint32_t lo, uint32_t hi) {
   return mh & ~((1u << (8u * l)) - 1u);
 }
 
-template <class G>
-XYWS_DEV u32x4 chunk_xor(const lds_t<G>& L, uint32_t nfl, uint32_t g, uint32_t a) {
+XYWS_DEV u32x4 chunk_xor(const fent* fl, uint32_t nfl, uint32_t g, uint32_t a) {
   u32x4 w = {0u, 0u, 0u, 0u};
   for (uint32_t h = g; h < nfl; h++) {
-    const fent f = L.fl[h];
+    const fent f = fl[h];
     if (h != g && f.start >= a + 16) break;
     w.x |= f.kw & range_mask32(a, f.ps, f.end);
     w.y |= f.kw & range_mask32(a + 4, f.ps, f.end);
@@ -851,6 +854,7 @@ XYWS_DEV uint32_t stride_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uin
   const uint32_t n0 = S0.X > ss ? 1u : 0u;
   if (lane == 0 && n0) L.fl[0] = fent{0u, clamp_rel(S0.cov_ps, ss), clamp_rel(S0.X, ss), S0.cov_kw};
   uint32_t n = n0, total = 0, x = (uint32_t)(S0.X - ss), f = (uint32_t)F;
+  bool uni = true;  // every accepted frame F bytes long (lattice_check)
   cstate S = S0;
   for (;;) {
     // two positions per lane: frames x + lane*f (A) and x + (64 + lane)*f (B)
@@ -897,9 +901,11 @@ XYWS_DEV uint32_t stride_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uin
     total += a;
     x = lp + lhl + lpl;
     f = lhl + lpl;
+    uni = uni && f == (uint32_t)F;
     if (a < STRIDE_MIN || x >= st || n >= G::FCAP) break;
   }
   if (lane == 0) {
+    L.ar_f = uni ? (uint32_t)F : 0u;
     if (total) {
       L.S = S;
       L.cnt += total;
@@ -1162,7 +1168,7 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
 // before the row (binary search).
 constexpr uint32_t ROW_FAST = 1u << 16, ROW_SKIP = 1u << 17;
 template <class G>
-XYWS_DEV void build_rows(lds_t<G>& L, uint32_t nfl, uint32_t lo_c, uint32_t hi_c, uint32_t wl_r,
+XYWS_DEV void build_rows(const fent* fl, uint2* rt, uint32_t nfl, uint32_t lo_c, uint32_t hi_c, uint32_t wl_r,
                          uint32_t wh_r, bool any, uint32_t lane) {
   for (uint32_t r = lane; r < G::SEG / 1024; r += 64) {
     const uint32_t R0 = r * 1024, R1 = R0 + 1024;
@@ -1171,17 +1177,17 @@ XYWS_DEV void build_rows(lds_t<G>& L, uint32_t nfl, uint32_t lo_c, uint32_t hi_c
       uint32_t x = 0, y = nfl;
       while (y - x > 1) {
         const uint32_t mid = (x + y) >> 1;
-        if (L.fl[mid].start <= R0) x = mid; else y = mid;
+        if (fl[mid].start <= R0) x = mid; else y = mid;
       }
-      const fent e = L.fl[x];
-      const uint32_t ns = x + 1 < nfl ? L.fl[x + 1].start : 0xFFFFFFFFu;
+      const fent e = fl[x];
+      const uint32_t ns = x + 1 < nfl ? fl[x + 1].start : 0xFFFFFFFFu;
       info = x;
       if (R0 >= lo_c && R1 <= hi_c && R0 >= wl_r && R1 <= wh_r && e.ps <= R0 && e.end >= R1 && ns >= R1) {
         info = e.kw ? ROW_FAST : ROW_SKIP;
         kw = e.kw;
       }
     }
-    L.rt[r] = uint2{info, kw};
+    rt[r] = uint2{info, kw};
   }
 }
 
@@ -1198,8 +1204,8 @@ XYWS_DEV void build_rows(lds_t<G>& L, uint32_t nfl, uint32_t lo_c, uint32_t hi_c
 // the store loop). chunk_of(k, a, r, ok): the lane's k-th chunk offset, its
 // 1 KiB row, and whether it exists.
 template <class G, uint32_t NK, class ChunkOf>
-XYWS_DEV uint32_t boundary_chunks(lds_t<G>& L, uint32_t nfl, uint32_t lo_c, uint32_t hi_c, uint32_t wl_r,
-                                  uint32_t wh_r, ChunkOf chunk_of, uint32_t& edge) {
+XYWS_DEV uint32_t boundary_chunks(lds_t<G>& L, const fent* fl, const uint2* rt, uint32_t nfl, uint32_t lo_c,
+                                  uint32_t hi_c, uint32_t wl_r, uint32_t wh_r, ChunkOf chunk_of, uint32_t& edge) {
   // the rows' classes first, all reads issued at once (one LDS round trip:
   // rows of whole-frame payload, the large-frame case, cost nothing more)
   uint32_t need = 0;
@@ -1208,10 +1214,11 @@ XYWS_DEV uint32_t boundary_chunks(lds_t<G>& L, uint32_t nfl, uint32_t lo_c, uint
     uint32_t a = 0, r = 0;
     bool ok = false;
     chunk_of(k, a, r, ok);
-    const uint32_t info = __builtin_amdgcn_readfirstlane(L.rt[r].x);
+    const uint32_t info = __builtin_amdgcn_readfirstlane(rt[r].x);
     if (ok && !(info & (ROW_FAST | ROW_SKIP))) need |= 1u << k;
   }
   uint32_t put = 0;
+  const uint32_t lane = __lane_id();
 #pragma nounroll
   while (need) {
     const uint32_t k = __builtin_ctz(need);
@@ -1219,18 +1226,57 @@ XYWS_DEV uint32_t boundary_chunks(lds_t<G>& L, uint32_t nfl, uint32_t lo_c, uint
     uint32_t a = 0, r = 0;
     bool ok = false;
     chunk_of(k, a, r, ok);
-    if (!(a >= lo_c && a < hi_c && a + 16 > wl_r && a < wh_r)) continue;
-    if (!(a >= wl_r && a + 16 <= wh_r)) {
-      edge |= 1u << k;
-      continue;
+    // The row's frames at once (the wave holds one row: lane = chunk): lane j
+    // reads entry g0 + j (g0 = the row's first entry, from the row table);
+    // lane c's chunk starts in the last entry starting at or before it (g) and
+    // meets every entry up to the last one starting before its end (gh): both
+    // from the starts, broadcast one per step (no LDS round trip per entry).
+    const uint32_t g0 = __builtin_amdgcn_readfirstlane(rt[r].x), R1 = r * 1024u + 1024u;
+    const fent ej = g0 + lane < nfl ? fl[g0 + lane] : fent{0xFFFFFFFFu, 0u, 0u, 0u};
+    const uint64_t inrow = __ballot(lane >= 1 && ej.start < R1);
+    const bool mine = a >= lo_c && a < hi_c && a + 16 > wl_r && a < wh_r;
+    const bool whole = a >= wl_r && a + 16 <= wh_r;
+    if (mine && !whole) edge |= 1u << k;
+    u32x4 m = {0u, 0u, 0u, 0u};
+    if (inrow >> 63) {
+      // (64 entries or more in the row: tiny frames) the walk from g0
+      uint32_t g = g0;
+      uint32_t ns = g + 1 < nfl ? fl[g + 1].start : 0xFFFFFFFFu;
+      while (ns <= a) {
+        g++;
+        ns = g + 1 < nfl ? fl[g + 1].start : 0xFFFFFFFFu;
+      }
+      if (mine && whole) m = chunk_xor(fl, nfl, g, a);
+    } else {
+      uint32_t g = 0, gh = 0;
+      for (uint64_t b = inrow; b; b &= b - 1) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(b);
+        const uint32_t sj = __builtin_amdgcn_readlane(ej.start, j);
+        if (sj <= a) g = j;
+        if (sj < a + 16) gh = j;
+      }
+      const fent f0 = fl[g0 + g];
+      const fent f1 = fl[g0 + g + (gh > g ? 1u : 0u)];
+      m.x = f0.kw & range_mask32(a, f0.ps, f0.end);
+      m.y = f0.kw & range_mask32(a + 4, f0.ps, f0.end);
+      m.z = f0.kw & range_mask32(a + 8, f0.ps, f0.end);
+      m.w = f0.kw & range_mask32(a + 12, f0.ps, f0.end);
+      if (gh > g) {
+        m.x |= f1.kw & range_mask32(a, f1.ps, f1.end);
+        m.y |= f1.kw & range_mask32(a + 4, f1.ps, f1.end);
+        m.z |= f1.kw & range_mask32(a + 8, f1.ps, f1.end);
+        m.w |= f1.kw & range_mask32(a + 12, f1.ps, f1.end);
+        // (a third frame starting in the chunk: frames under 16 bytes)
+        for (uint32_t h = g0 + g + 2; h <= g0 + gh; h++) {
+          const fent f = fl[h];
+          m.x |= f.kw & range_mask32(a, f.ps, f.end);
+          m.y |= f.kw & range_mask32(a + 4, f.ps, f.end);
+          m.z |= f.kw & range_mask32(a + 8, f.ps, f.end);
+          m.w |= f.kw & range_mask32(a + 12, f.ps, f.end);
+        }
+      }
+      if (!(mine && whole)) m = u32x4{0u, 0u, 0u, 0u};
     }
-    uint32_t g = L.rt[r].x;
-    uint32_t ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
-    while (ns <= a) {
-      g++;
-      ns = g + 1 < nfl ? L.fl[g + 1].start : 0xFFFFFFFFu;
-    }
-    const u32x4 m = chunk_xor(L, nfl, g, a);
     if (m.x | m.y | m.z | m.w) {
       u32x4* c = reinterpret_cast<u32x4*>(&L.seg[a]);
       *c = *c ^ m;
@@ -1362,6 +1408,45 @@ XYWS_DEV void answer_split(const run_params& P, lds_t<G>& L, uint64_t ss, uint64
 // L.rng_end, unless known). The chase stops at the successor's W; L.ok tells
 // whether it landed on its entry. A run (L.victim) answers steal requests on
 // the way: its range end shrinks to the split.
+// Lattice passes (run_chain; wave 0, after the chase of a single pass over the
+// whole segment): when the list's entries 1, 2, ... start at X0, X0 + F, X0 +
+// 2F, ... (equal frames, F >= 16: the stride pass's streams), the entry a
+// chunk starts in is arithmetic, g = 1 + (a - X0) / F (0 before X0), and the
+// chunk meets at most one more (g + 1): the store loop reads those two entries
+// instead of the row table and the per-chunk walk (no row table is built).
+// The stride pass's entries (below k0) are on the lattice when every frame it
+// accepted was F bytes long (L.ar_f = F); the chase's few after them are
+// checked here.
+template <class G>
+XYWS_DEV bool lattice_check(lds_t<G>& L, uint32_t nfl, uint32_t k0, uint32_t lane) {
+  const uint32_t f = L.ar_f;
+  if (nfl < 3 || f < 16 || f > G::SEG) return false;
+  const uint32_t x0 = L.fl[1].start;
+  if (L.fl[2].start - x0 != f) return false;
+  bool ok = true;
+  for (uint32_t i = (k0 > 1 ? k0 : 1u) + lane; i < nfl; i += 64) ok = ok && L.fl[i].start == x0 + (i - 1) * f;
+  if (__ballot(!ok)) return false;
+  if (lane == 0) L.ar_x0 = x0;
+  return true;
+}
+
+// The two entries of chunk a on the lattice (x0, f; nfl entries): g, and
+// whether entry g + 1 starts in the chunk.
+XYWS_DEV uint32_t lattice_entry(uint32_t a, uint32_t x0, uint32_t f, float inv, uint32_t nfl, bool& two) {
+  uint32_t g = 0;
+  if (a >= x0) {
+    const uint32_t d = a - x0;
+    uint32_t i = (uint32_t)((float)d * inv);
+    if ((i + 1) * f <= d) i++;
+    else if (i * f > d) i--;
+    g = 1 + i;
+  }
+  if (g > nfl - 1) g = nfl - 1;
+  const uint32_t nxs = g == 0 ? x0 : x0 + g * f;  // entry g + 1's start
+  two = g + 1 < nfl && nxs < a + 16;
+  return g;
+}
+
 template <class G>
 XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint64_t ss0,
                         bool in_lds, uint64_t wlo) {
@@ -1486,7 +1571,11 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint64_t t_r1 = st_on ? __builtin_amdgcn_s_memtime() : 0;
-        build_rows<G>(L, L.nfl, lo_c, L.pass_hi, wl_r, wh_r, any, tid);
+        // (only after a stride pass: mixed sizes skip the check)
+        const bool lat = k0 != 0 && lo_c == 0 && L.pass_hi >= G::SEG && !(P.opts & XYWS_OPT_NO_LATTICE) &&
+                         lattice_check<G>(L, L.nfl, k0, tid);
+        if (tid == 0) L.ar = lat;
+        if (!lat) build_rows<G>(L.fl, L.rt, L.nfl, lo_c, L.pass_hi, wl_r, wh_r, any, tid);
         if (st_on && tid == 0) {
           stat_add(P, ST_T_SER, t_r1 - t_r0);
           stat_add(P, ST_T_ROWS, __builtin_amdgcn_s_memtime() - t_r1);
@@ -1511,8 +1600,42 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
       // this unrolled loop: the next segment's loads are in flight).
       uint32_t edge = 0;
       const uint32_t wave = tid >> 6;
+      if (L.ar) {
+        // a lattice pass: each chunk's two entries by arithmetic (lattice_entry)
+        const uint32_t x0 = L.ar_x0, f = L.ar_f;
+        const float inv = 1.0f / (float)f;
+        u32x4 dprev = {0u, 0u, 0u, 0u};
+#pragma unroll 2
+        for (uint32_t k = 0; k < G::CH; k++) {
+          const uint32_t a = (k * G::NT + tid) * 16u;
+          bool two = false;
+          const uint32_t g = lattice_entry(a, x0, f, inv, nfl, two);
+          const fent f0 = L.fl[g];
+          const fent f1 = L.fl[two ? g + 1 : g];
+          const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
+          u32x4 m;
+          m.x = f0.kw & range_mask32(a, f0.ps, f0.end);
+          m.y = f0.kw & range_mask32(a + 4, f0.ps, f0.end);
+          m.z = f0.kw & range_mask32(a + 8, f0.ps, f0.end);
+          m.w = f0.kw & range_mask32(a + 12, f0.ps, f0.end);
+          if (two) {
+            m.x |= f1.kw & range_mask32(a, f1.ps, f1.end);
+            m.y |= f1.kw & range_mask32(a + 4, f1.ps, f1.end);
+            m.z |= f1.kw & range_mask32(a + 8, f1.ps, f1.end);
+            m.w |= f1.kw & range_mask32(a + 12, f1.ps, f1.end);
+          }
+          const bool whole = a >= wl_r && a + 16 <= wh_r;
+          if (!whole && a + 16 > wl_r && a < wh_r) edge |= 1u << k;
+          const uint32_t off = whole && (m.x | m.y | m.z | m.w) ? tid * 16u : OOB;
+          const u32x4 d = v ^ m;
+          __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, k * G::NT * 16u, AUX_ST);
+          asm volatile("" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
+          dprev = d;
+        }
+        asm volatile("s_nop 1" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
+      } else {
       const uint32_t put = boundary_chunks<G, G::CH>(
-          L, nfl, lo_c, hi_c, wl_r, wh_r,
+          L, L.fl, L.rt, nfl, lo_c, hi_c, wl_r, wh_r,
           [&](uint32_t k, uint32_t& a, uint32_t& r, bool& ok) {
             a = (k * G::NT + tid) * 16u;
             r = k * (G::NT / 64) + wave;
@@ -1560,6 +1683,7 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
         dprev = d;
       }
       asm volatile("s_nop 1" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
+      }
 #pragma nounroll
       while (edge) {  // chunks with a frame boundary, and the batch's first/last chunk
         const uint32_t k = __builtin_ctz(edge);
@@ -1570,7 +1694,7 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
           const uint32_t mid = (x + y) >> 1;
           if (L.fl[mid].start <= a) x = mid; else y = mid;
         }
-        const u32x4 m = chunk_xor(L, nfl, x, a);
+        const u32x4 m = chunk_xor(L.fl, nfl, x, a);
         if ((m.x | m.y | m.z | m.w) == 0u) continue;
         if (a >= wl_r && a + 16 <= wh_r) {
           const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
@@ -2831,9 +2955,7 @@ XYWS_DEV void sweep_scan(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   const uint32_t qlim = rel_hi < G::SEG ? (uint32_t)rel_hi : G::SEG;
   uint32_t done = 0;  // survivors already checked
   __syncthreads();
-  uint32_t win = 0;
   for (uint32_t k = 0; k < nwin && k < G::CH; k++) {
-    win++;
     const uint32_t a = (k * G::NT + tid) * 16u;
     uint32_t c = 0;
     if (a < qlim) {
@@ -2935,7 +3057,7 @@ XYWS_DEV void store_pass(const run_params& P, const lds_t<G>& L, uint64_t ss, ui
   uint32_t edge = 0;
   const uint32_t wave = tid >> 6;
   const uint32_t put = boundary_chunks<G, G::CH>(
-      const_cast<lds_t<G>&>(L), nfl, lo_c, hi_c, wl_r, wh_r,
+      const_cast<lds_t<G>&>(L), L.fl, L.rt, nfl, lo_c, hi_c, wl_r, wh_r,
       [&](uint32_t k, uint32_t& a, uint32_t& r, bool& ok) {
         a = (k * G::NT + tid) * 16u;
         r = k * (G::NT / 64) + wave;
@@ -2986,7 +3108,7 @@ XYWS_DEV void store_pass(const run_params& P, const lds_t<G>& L, uint64_t ss, ui
       const uint32_t mid = (x + y) >> 1;
       if (L.fl[mid].start <= a) x = mid; else y = mid;
     }
-    const u32x4 m = chunk_xor(L, nfl, x, a);
+    const u32x4 m = chunk_xor(L.fl, nfl, x, a);
     if ((m.x | m.y | m.z | m.w) == 0u) continue;
     if (a >= wl_r && a + 16 <= wh_r) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
@@ -3043,7 +3165,7 @@ struct sweep_io {
   // first loads, as the stores after every later segment's loads
   template <bool CHK = true>
   XYWS_DEV static void dummy(const run_params& P, uint64_t ss, uint32_t tid) {
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (CHK && !data_wave(wave)) return;
     const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss);
 #pragma unroll
@@ -3066,15 +3188,16 @@ struct sweep_io {
 // 16-byte store per chunk (skipped ones to the out-of-range offset), then the
 // chunks holding a frame boundary or a write-window edge (store_pass).
 template <class G, bool CHK = true>
-XYWS_DEV void store_rows(const run_params& P, const lds_t<G>& L, uint64_t ss, uint32_t tid, uint32_t nfl,
-                         uint32_t hi_c, uint64_t wl, uint64_t whi, uint32_t wl_r, uint32_t wh_r) {
+XYWS_DEV void store_rows(const run_params& P, const lds_t<G>& L, const fent* fl, const uint2* rt, uint64_t ss,
+                         uint32_t tid, uint32_t nfl, uint32_t hi_c, uint64_t wl, uint64_t whi, uint32_t wl_r,
+                         uint32_t wh_r) {
   using IO = sweep_io<G>;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
   if (CHK && !IO::data_wave(wave)) return;
   const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss);
   uint32_t edge = 0;
   const uint32_t put = boundary_chunks<G, IO::K>(
-      const_cast<lds_t<G>&>(L), nfl, 0u, hi_c, wl_r, wh_r,
+      const_cast<lds_t<G>&>(L), fl, rt, nfl, 0u, hi_c, wl_r, wh_r,
       [&](uint32_t k, uint32_t& a, uint32_t& r, bool& ok) {
         ok = IO::valid(wave, k);
         r = ok ? IO::row(wave, k) : 0u;
@@ -3088,7 +3211,7 @@ XYWS_DEV void store_rows(const run_params& P, const lds_t<G>& L, uint64_t ss, ui
     const bool ok = IO::valid(wave, k);
     const uint32_t r = ok ? IO::row(wave, k) : 0u;
     const uint32_t a = r * 1024u + lane * 16u;
-    const uint2 rw = L.rt[r];
+    const uint2 rw = rt[r];
     const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
     const uint32_t info = __builtin_amdgcn_readfirstlane(rw.x);
     const uint32_t kw = __builtin_amdgcn_readfirstlane(rw.y);
@@ -3121,9 +3244,9 @@ XYWS_DEV void store_rows(const run_params& P, const lds_t<G>& L, uint64_t ss, ui
     uint32_t x = 0, y = nfl;
     while (y - x > 1) {
       const uint32_t mid = (x + y) >> 1;
-      if (L.fl[mid].start <= a) x = mid; else y = mid;
+      if (fl[mid].start <= a) x = mid; else y = mid;
     }
-    const u32x4 m = chunk_xor(L, nfl, x, a);
+    const u32x4 m = chunk_xor(fl, nfl, x, a);
     if ((m.x | m.y | m.z | m.w) == 0u) continue;
     if (a >= wl_r && a + 16 <= wh_r) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
@@ -3183,7 +3306,7 @@ XYWS_DEV bool seg_passes(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (stores) build_rows<G>(L, L.nfl, lo_c, L.pass_hi, wl_r, wh_r, any, tid);
+      if (stores) build_rows<G>(L.fl, L.rt, L.nfl, lo_c, L.pass_hi, wl_r, wh_r, any, tid);
     }
     if (stores) {
       if (!dense) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3216,7 +3339,7 @@ XYWS_DEV void seg_store_list(const run_params& P, lds_t<G>& L, uint64_t ss, uint
   const uint32_t wl_r = wl > ss ? (wl - ss < G::SEG ? (uint32_t)(wl - ss) : G::SEG) : 0u;
   const uint32_t wh_r = whi > ss ? (whi - ss < G::SEG ? (uint32_t)(whi - ss) : G::SEG) : 0u;
   const bool any = !(P.opts & XYWS_OPT_NO_STORE) && wl_r < wh_r;
-  if (tid < 64) build_rows<G>(L, L.nfl, 0u, G::SEG, wl_r, wh_r, any, tid);
+  if (tid < 64) build_rows<G>(L.fl, L.rt, L.nfl, 0u, G::SEG, wl_r, wh_r, any, tid);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   store_pass<G>(P, L, ss, tid, L.nfl, 0u, G::SEG, wl, whi, wl_r, wh_r);
@@ -3430,7 +3553,7 @@ XYWS_DEV uint32_t sweep_slow(const run_params& P, lds_t<G>& L, uint32_t tid, uin
 enum { SWR_ALL = 0, SWR_CTRL = 1, SWR_DATA = 2 };
 template <class G, int ROLE>
 XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, uint64_t s, sweep_io<G>& io,
-                                uint32_t cr[5], uint32_t& claimed, uint64_t nx) {
+                                const uint32_t cr[5], uint32_t& claimed, uint64_t nx) {
   constexpr bool CT = ROLE != SWR_DATA, DT = ROLE != SWR_CTRL;
   const uint64_t ss = s * G::SEG;
   const uint64_t E = L.E;
@@ -3487,14 +3610,6 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
       }
     }
     L.sw_fast = fast;
-    // the prediction for the next segment (its predecessor header is loaded
-    // with its bytes)
-    L.sw_pcur = NONE;
-    if (nx < P.nseg) {
-      const uint64_t pn = pred_pos(L.sw_ref, L.sw_fsz, nx * G::SEG);
-      L.sw_pcur = pn;  // (consumed when the next segment starts: see the loop)
-      L.sw_fcur = L.sw_fsz;
-    }
     if (st_on) L.sw_t[1] += __builtin_amdgcn_s_memtime() - tq;
   }
   // the next segment's loads (wave 0 after its work above; lane 0's claim and
@@ -3507,8 +3622,6 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
       // for (inline asm: the compiler's atomic optimizer would wait for it,
       // and for this segment's stores, at once)
       asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(claimed) : "v"(P.head), "v"(1u) : "memory");
-      const uint64_t pn = L.sw_pcur;
-      if (pn != NONE && pn >= L.sw_fcur) cover_load(P, pn - L.sw_fcur, cr);
     }
     if constexpr (DT) io.template issue<ROLE == SWR_ALL>(P, nx * G::SEG, tid);
   }
@@ -3524,7 +3637,7 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
       const uint32_t wl_r = wl > ss ? (wl - ss < G::SEG ? (uint32_t)(wl - ss) : G::SEG) : 0u;
       const uint32_t wh_r = whi > ss ? (whi - ss < G::SEG ? (uint32_t)(whi - ss) : G::SEG) : 0u;
       const bool any = !(P.opts & XYWS_OPT_NO_STORE) && wl_r < wh_r;
-      build_rows<G>(L, L.nfl, 0u, G::SEG, wl_r, wh_r, any, tid);
+      build_rows<G>(L.fl, L.rt, L.nfl, 0u, G::SEG, wl_r, wh_r, any, tid);
     }
     if (tid == 0 && stats_on(P)) L.sw_t[2] += __builtin_amdgcn_s_memtime() - tb0;
   }
@@ -3556,7 +3669,7 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
         for (uint32_t r = tid; r < G::SEG / 1024; r += 64) L.rt[r] = uint2{ROW_SKIP, 0u};
       } else if (!fast) {
         const bool any = !(P.opts & XYWS_OPT_NO_STORE) && wl_r < wh_r;
-        build_rows<G>(L, L.nfl, 0u, G::SEG, wl_r, wh_r, any, tid);
+        build_rows<G>(L.fl, L.rt, L.nfl, 0u, G::SEG, wl_r, wh_r, any, tid);
       }
     }
     const uint64_t tl0 = swt_now(P);
@@ -3566,9 +3679,11 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
     if (tid == 64 && stats_on(P)) L.sw_t[4] += __builtin_amdgcn_s_memtime() - tl0;
     __syncthreads();
     const uint64_t ts0 = swt_now(P);
-    if constexpr (DT)
-      store_rows<G, ROLE == SWR_ALL>(P, L, ss, tid, act == SW_REUSE ? L.nfl : 0u, act == SW_REUSE ? G::SEG : 0u, wl,
-                                     whi, wl_r, wh_r);
+    if constexpr (DT) {
+      store_rows<G, ROLE == SWR_ALL>(P, L, L.fl, L.rt, ss, tid,
+                                     act == SW_REUSE ? L.nfl : 0u, act == SW_REUSE ? G::SEG : 0u, wl, whi,
+                                     wl_r, wh_r);
+    }
     if (tid == 64 && stats_on(P)) L.sw_t[5] += __builtin_amdgcn_s_memtime() - ts0;
     // the control wave checks the previous predicted segment while the data
     // waves store (its look-back waits for memory: off the stores' path)
@@ -3578,6 +3693,7 @@ XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, 
         sweep_validate(P, vs, vs * G::SEG, E, tid, L.sw_vU);
         if (tid == 0) L.sw_vs = NONE;
       }
+      // the next segment's list from the headers loaded in B
     }
   }
   __syncthreads();
@@ -3749,7 +3865,9 @@ XYWS_DEV uint64_t sweep_loop(const run_params& P, lds_t<G>& L, uint32_t tid0, ui
   uint32_t tid = tid0;
   asm volatile("" : "+v"(tid));
   sweep_io<G> io;
-  uint32_t cr[5] = {0u, 0u, 0u, 0u, 0u};  // lane 0: its predicted predecessor header (sweep_predicted)
+  // lane 0: the predicted predecessor header of this segment and of the next
+  // (sweep_predicted)
+  uint32_t cr[5] = {0u, 0u, 0u, 0u, 0u}, crn[5] = {0u, 0u, 0u, 0u, 0u};
   uint64_t frames = 0;                     // lane 0
   uint64_t cur = uniform64(L.sw_cur);
   if (DT && cur < P.nseg) {
@@ -3775,12 +3893,27 @@ XYWS_DEV uint64_t sweep_loop(const run_params& P, lds_t<G>& L, uint32_t tid0, ui
       // the segment claimed during the previous segment (lane 0's atomic:
       // wave 0 waits for its own few memory operations)
       asm volatile("s_waitcnt vmcnt(0)" : "+v"(claimed)::"memory");
-      L.sw_next = claimed < P.nseg ? claimed : NONE;
+      const uint64_t nx = claimed < P.nseg ? claimed : NONE;
+      L.sw_next = nx;
+      // the stride prediction for the next segment, and its predecessor's
+      // header: loaded before the data waves issue the next segment's bytes,
+      // so that they return ahead of them
+      L.sw_pcur = L.sw_pnx;  // (this segment's, made one segment ago)
+      L.sw_fcur = L.sw_fnx;
+      L.sw_pnx = NONE;
+      if (nx < P.nseg) {
+        const uint64_t pn = pred_pos(L.sw_ref, L.sw_fsz, nx * G::SEG);
+        L.sw_pnx = pn;
+        L.sw_fnx = L.sw_fsz;
+        if (pn != NONE && pn >= L.sw_fsz) cover_load(P, pn - L.sw_fsz, crn);
+      }
       if (stats_on(P)) L.sw_t[0] += __builtin_amdgcn_s_memtime() - tc0;
     }
     __syncthreads();
     const uint64_t nx = uniform64(L.sw_next);
     frames += sweep_segment<G, ROLE>(P, L, tid, cur, io, cr, claimed, nx);
+#pragma unroll
+    for (int i = 0; i < 5; i++) cr[i] = crn[i];
     if (tid == 64 && stats_on(P)) L.sw_t[7] += __builtin_amdgcn_s_memtime() - ti0;
     cur = nx;
   }
@@ -3806,6 +3939,8 @@ __global__ void __launch_bounds__(G::NT, G::WPE) k_stream_sweep(run_params P) {
     L.sw_fsz = 0;
     L.sw_pcur = NONE;
     L.sw_fcur = 0;
+    L.sw_pnx = NONE;
+    L.sw_fnx = 0;
     L.sw_vs = NONE;
     L.sw_fsmin = ~0ull;
     L.sw_fsmax = 0;
