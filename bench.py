@@ -703,7 +703,8 @@ def main():
     if args.mode == "fused":
         pol = (C.c_uint64 * 5)()
         if dec.ctx.L.xyws_debug_policy(dec.ctx.h, C.c_void_p(stream.cuda_stream), pol) == 0:
-            decoder = ["runs (k_stream_runs)", "sweep (k_stream_sweep)"][int(pol[4]) & 1]
+            decoder = {0: "runs (k_stream_runs)", 1: "sweep (k_stream_sweep)",
+                       2: "runs (k_stream_runs, 512-thread workgroups, 64 KiB segments)"}.get(int(pol[4]) & 3)
 
     if args.stats and rank == 0:  # two extra decodes of copy 0 (keeps its parity)
         names = ["runs", "runs_without_entry", "bad_boundaries", "repairs", "cuts", "spins", "dense_passes",
@@ -724,6 +725,8 @@ def main():
         if decoder and decoder.startswith("sweep"):  # (the sweep's own timing split: ST_SWT_*, per segment)
             names[16:26] = ["cyc_claim_wait", "cyc_phase_a", "cyc_phase_b", "cyc_data_barrier", "cyc_data_load",
                             "cyc_records", "cyc_data_store", "cyc_data_fill", "cyc_iteration", "cyc_predict"]
+        else:
+            names[46] = "cyc_stride_pass"
         st = {k: v for k, v in zip(names, list(out))}
         nrun = max(1, (st["dense_passes"] if decoder and decoder.startswith("sweep") else st["runs"] + 1))
         for k in list(st):

@@ -266,6 +266,57 @@ def test_stride_pass_adversarial(ws, oracle, mode, kind):
         assert r2.nframes == on and host(view2) == ob.tobytes()
 
 
+def test_lattice_entry_follows_the_previous_call(ws, oracle):
+    """The run decoder's lattice entry (find_entry): after a call whose frames
+    were all F bytes long, each run first tries the frame start the lattice
+    X0 + kF gives (X0: the batch's first frame). Three calls on one stream:
+    equal 264-byte frames twice (sets F = 264; the next calls run in 512-thread
+    workgroups; the second takes the lattice entries), then a batch whose first frame is 308 bytes and whose
+    payloads hold valid 264-byte headers exactly on the lattice from 0 (every
+    run's lattice entry is plausible and wrong: the hand-overs repair it),
+    then 520-byte frames (the lattice header has the wrong size: the scan).
+    GPU vs oracle: bytes, count, descriptors, carry, for each call."""
+    rng = streams.SplitMix(0x1A77)
+    target = 8 << 20
+    regular = bytearray()
+    while len(regular) < target:
+        regular += streams.frame(rng, 0x82, 256)
+    fakes = bytearray(streams.frame(rng, 0x82, 300))
+    while len(fakes) < target:
+        fakes += streams.frame(rng, 0x82, 256)
+    fake = streams.header(0x82, 256, rng.bytes(4))
+    assert len(fake) + 256 == 264
+    for k in range(1, len(fakes) // 264):
+        o = 264 * k
+        if o + len(fake) <= len(fakes):
+            fakes[o:o + len(fake)] = fake
+    other = bytearray()
+    while len(other) < target:
+        other += streams.frame(rng, 0x82, 512)
+    from xynet_amd import _lib
+    stream = torch.cuda.current_stream()
+    st = []
+    for src in (bytes(regular), bytes(regular), bytes(fakes), bytes(other)):
+        # (a new decoder per batch: a fresh carry; the policy words belong to
+        # the stream's scratch and stay)
+        dec = ws.frame_decoder(opts=_lib.OPT_STATS)
+        view, _ = dev_bytes(src)
+        ob = np.frombuffer(src, np.uint8).copy()
+        ofr, carry, on = oracle.decode_stream(ob, cap=len(src) // 8 + 2)
+        r = dec.decode(view, cap=on + 2)
+        assert r.nframes == on
+        assert host(view) == ob.tobytes()
+        assert frames_list(r.frames(), True) == frames_list(ofr, True)
+        assert carry_list(dec.carry()) == carry_list(carry)
+        assert dec.ctx.last_device_error() == 0
+        out = (C.c_uint64 * _lib.NSTATS)()
+        assert dec.ctx.L.xyws_debug_stats(dec.ctx.h, C.c_void_p(stream.cuda_stream), out) == 0
+        st.append(list(out))
+    assert st[1][_lib.ST_P_LATTICE] > 0 and st[1][_lib.ST_BAD] == 0  # right: every lattice entry holds
+    assert st[2][_lib.ST_P_LATTICE] > 0 and st[2][_lib.ST_BAD] > 0   # plausible and wrong: repaired
+    assert st[3][_lib.ST_P_LATTICE] == 0                             # wrong size: scanned
+
+
 # --------------------------------------------------------------------------- indexed
 def test_indexed_matches_golden(ws):
     g = load_golden("streams.json")["cases"]["lengths"]

@@ -278,8 +278,10 @@ def test_decoder_choice_follows_the_frames(ws):
     """The decoder choice (stream_decode_fused: sweep_preferred): a call
     without descriptors takes the sweep decoder when the previous call on the
     stream found regular frames of 16 KiB or more (config 3), the run decoder
-    otherwise (config 4's irregular frames, config 2's 256 B ones). Every call
-    is checked against the reference's digests, whichever decoder ran."""
+    otherwise (config 4's irregular frames, config 2's 256 B ones), in 512-thread
+    workgroups after regular frames under 2 KiB (wg512_preferred: policy word
+    2). Every call is checked against the reference's digests, whichever
+    decoder ran."""
     from xynet_amd import _lib
     seq = [("c3_bin_64k", 0), ("c3_bin_64k", 0), ("c3_bin_64k", 0), ("c4_mixed", 0), ("c4_mixed", 0),
            ("c2_bin_256", 0), ("c2_bin_256", 0), ("c3_bin_64k", _lib.OPT_RUNS)]
@@ -307,5 +309,6 @@ def test_decoder_choice_follows_the_frames(ws):
     assert used[3] == 1                           # the first c4 call follows c3's statistics...
     assert pols[3][2] < pols[3][3]                # ...and finds irregular frames
     assert used[4] == 0                           # so the next one takes the run decoder
-    assert pols[5][2] == pols[5][3] == 264 and used[6] == 0  # 256 B frames: runs
-    assert used[7] == 0                           # XYWS_OPT_RUNS forces the run decoder
+    assert used[5] == 0                           # after c4's irregular frames: runs, 1024-thread workgroups
+    assert pols[5][2] == pols[5][3] == 264 and used[6] == 2  # 256 B frames: runs, 512-thread workgroups
+    assert used[7] & 1 == 0                       # XYWS_OPT_RUNS forces the run decoder

@@ -20,6 +20,8 @@ R_WORDS = 32  # u64 words per run record (xyws_stream.hip)
 OPT_STATS = 0x100
 OPT_SMALL_SEG = 0x200
 OPT_WG512 = 0x40000
+OPT_NO_LATENTRY = 0x4000   # run decoder experiment: no lattice entry
+OPT_WG1024 = 0x8000        # the run decoder's default geometry, whatever the geometry choice would take
 OPT_TEST_GIVEUP = 0x100000
 OPT_STEAL = 0x400000
 OPT_TEST_STEAL = 0x800000
@@ -33,6 +35,7 @@ ST_GIVEUP, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS = 32, 33, 34, 35
 # decode (a partial header), deferred to the repair walk; look-back / scan /
 # speculation cycles; scan windows
 ST_SW_APPLY, ST_SW_NOTHING, ST_SW_TLB, ST_SW_TSCAN, ST_SW_TSPEC, ST_SW_DEFER, ST_SW_WIN = range(40, 47)
+ST_P_LATTICE = 40  # run decoder: runs whose entry the lattice gave (find_entry; the sweep's ST_SW_APPLY slot)
 ERRORS = {-1: "invalid argument", -2: "HIP runtime error", -3: "device allocation failed",
           -4: "scratch capacity exceeded", -5: "device-side error", -6: "not complete yet"}
 

@@ -417,7 +417,7 @@ int64_t xyws_debug_records(xyws_ctx* ctx, void* stream, uint64_t* out, uint64_t 
 
 // Internal: the decoder-choice words the last fused stream decode on `stream`
 // published ({epoch, batch bytes, smallest, largest last-frame size, decoder:
-// 0 runs / 1 sweep}). Synchronizes the device.
+// 0 runs / 1 sweep / 2 runs in 512-thread workgroups}). Synchronizes the device.
 int xyws_debug_policy(xyws_ctx* ctx, void* stream, uint64_t* out) {
   if (!ctx || !out) return XYWS_ERR_INVALID;
   std::lock_guard<std::mutex> lk(ctx->mu);

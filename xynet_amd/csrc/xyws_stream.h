@@ -40,6 +40,11 @@ int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_ru
 #define XYWS_OPT_STATS 0x100u      // count speculation/repair events (xyws_debug_stats)
 #define XYWS_OPT_SMALL_SEG 0x200u  // 1 KiB segments, one per run: exercises run-boundary
                                    // speculation and repair on small test inputs
+#define XYWS_OPT_NO_LATENTRY 0x4000u // experiment (run decoder): no lattice entry (find_entry scans every run)
+#define XYWS_OPT_WG1024 0x8000u    // the run decoder in its default geometry (one 1024-thread workgroup per CU),
+                                   // whatever the geometry choice (wg512_preferred) would take
+#define XYWS_OPT_RUNS_NOWAIT 0x10000u // experiment (run decoder): a serial-chase segment's stores do not wait for the
+                                   // next segment's loads (the dense pass's behaviour)
 #define XYWS_OPT_NO_STORE 0x20000u // diagnostics: decode without writing (timing split only)
 #define XYWS_OPT_WG512 0x40000u    // two 512-thread workgroups per CU, 64 KiB segments
 #define XYWS_OPT_DIAG 0x80000u     // diagnostics: no prefetch during the prologue scan (timing only)

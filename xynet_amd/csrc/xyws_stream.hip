@@ -240,6 +240,8 @@ struct run_params {
   uint64_t* split;        // per run: split word (2 x u64)
   uint64_t* prog;         // per run: (E << 24) | segment being decoded (thieves pick the run with most left)
   const xyws_carry* cin_user;  // caller's incoming carry (nullable; may alias cout)
+  uint64_t pfs;                // run decoder: the frame size the previous call's frames all had (0: none;
+                               // find_entry's lattice entry)
   xyws_carry* cin;        // private snapshot of it, written by run 0 (finish/emit read it)
   xyws_carry* cout;
   xyws_frame* frames;
@@ -329,7 +331,9 @@ enum { ST_RUNS = 0, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRA
        ST_P_WIN, ST_P_CAND, ST_P_UND, ST_P_TCOMP, ST_P_TCHECK, ST_P_TRES, ST_D_TENT, ST_D_TCHASE,
        ST_T_PRO = 16, ST_T_MAIN, ST_T_WAIT, ST_T_FILL, ST_T_CHASE, ST_T_XOR, ST_T_TAIL, ST_T_PF, ST_T_CP,
        ST_P_FILL, ST_P_SCAN, ST_P_PUB, ST_D_NOENT, ST_D_CHASE, ST_D_MISMATCH, ST_D_OVF,
-       ST_GIVEUP = 32, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS, ST_D_TVAL, ST_T_ROWS, ST_T_SER };
+       ST_GIVEUP = 32, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS, ST_D_TVAL, ST_T_ROWS, ST_T_SER,
+       ST_T_STRIDE = 46,    // (46: the sweep's ST_SW_WIN; the run decoder's stride-pass time)
+       ST_P_LATTICE = 40 }; // (40: the sweep's ST_SW_APPLY; runs whose entry the lattice gave)
 XYWS_DEV void stat_add(const run_params& P, uint32_t i, uint64_t v) {
   if (stats_on(P)) atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + i, (unsigned long long)v);
 }
@@ -817,13 +821,13 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
 // Stride pass (wave 0, every lane; the first pass of a segment, before lane
 // 0's serial chase). In a stream of equal frames the frame after X starts at
 // X + F, F the size of the frame that ends at X; lane i parses the headers at
-// X + i*F and X + (64 + i)*F from LDS (the serial chase's 32-bit parse,
-// below the same stop). Position 0 is exact (X); position i is exact when
+// X + (64j + i)*F, j < SP, from LDS (the serial chase's 32-bit parse, below
+// the same stop). Position 0 is exact (X); position i is exact when
 // positions 0..i-1 each hold a frame of exactly F bytes (induction from X),
 // so ONE ballot accepts positions 0..m, m the first whose frame is not F
 // bytes long (its start is exact too; its own size ends the step). A step
-// decides up to 128 frames in
-// one LDS round trip where the serial chase takes one hop per frame, and it
+// decides up to 64*SP frames in one LDS round trip where the serial chase
+// takes one hop per frame, and it
 // is exact whatever the bytes: no accepted position is a guess. Steps repeat
 // from the new X while one accepts STRIDE_MIN frames or more. Returns the
 // list entries written (the covering frame first, as chase_pass writes it;
@@ -831,6 +835,7 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
 // descriptor starts as chase_pass would: lane 0's serial chase continues
 // from there (limits, the segment end, lengths of 2^31 or more).
 constexpr uint32_t STRIDE_MIN = 8;
+constexpr uint32_t SP = 4;  // stride-pass positions per lane (up to 256 frames per step)
 template <class G>
 XYWS_DEV uint32_t stride_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t lane) {
   const cstate S0 = L.S;
@@ -857,40 +862,52 @@ XYWS_DEV uint32_t stride_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uin
   bool uni = true;  // every accepted frame F bytes long (lattice_check)
   cstate S = S0;
   for (;;) {
-    // two positions per lane: frames x + lane*f (A) and x + (64 + lane)*f (B)
-    const uint64_t pa64 = (uint64_t)x + (uint64_t)lane * f, pb64 = pa64 + 64ull * f;
-    const bool va = pa64 < st && n + lane < G::FCAP, vb = pb64 < st && n + 64 + lane < G::FCAP;
-    const uint32_t pa = (uint32_t)pa64, pb = (uint32_t)pb64;
-    uint32_t hla = 0, pla = 0, kya = 0, hlb = 0, plb = 0, kyb = 0, b01 = 0;
-    bool oka = false, okb = false;
-    if (va) oka = parse_rel<G>(L, pa, hla, pla, kya, b01);
-    if (vb) okb = parse_rel<G>(L, pb, hlb, plb, kyb, b01);
-    const uint64_t vma = __ballot(va), vmb = __ballot(vb);
-    const uint64_t oma = __ballot(oka), omb = __ballot(okb);
-    const uint64_t mma = __ballot(oka && hla + pla == f), mmb = __ballot(okb && hlb + plb == f);
-    // the first position without a match, in the sequence A then B
-    const uint32_t m = mma != ~0ull ? (uint32_t)__builtin_ctzll(~mma)
-                                    : 64u + (mmb == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~mmb));
-    const bool okm = m < 64 ? ((oma >> m) & 1ull) != 0 : (m < 128 && ((omb >> (m - 64)) & 1ull) != 0);
+    // SP positions per lane: frames x + (64*j + lane)*f, j < SP
+    uint32_t pj[SP], hl[SP], pl[SP], ky[SP];
+    uint64_t vm[SP], om[SP], mm[SP];
+#pragma unroll
+    for (uint32_t j = 0; j < SP; j++) {
+      const uint64_t p64 = (uint64_t)x + (uint64_t)(64u * j + lane) * f;
+      const bool v = p64 < st && n + 64u * j + lane < G::FCAP;
+      pj[j] = (uint32_t)p64;
+      hl[j] = pl[j] = ky[j] = 0;
+      uint32_t b01 = 0;
+      const bool ok = v && parse_rel<G>(L, pj[j], hl[j], pl[j], ky[j], b01);
+      vm[j] = __ballot(v);
+      om[j] = __ballot(ok);
+      mm[j] = __ballot(ok && hl[j] + pl[j] == f);
+    }
+    // the first position without a match, in the order j = 0, 1, ...
+    uint32_t m = 64u * SP, nv = 0;
+    bool okm = false;
+#pragma unroll
+    for (int j = SP - 1; j >= 0; j--)
+      if (mm[j] != ~0ull) {
+        m = 64u * j + (uint32_t)__builtin_ctzll(~mm[j]);
+        okm = ((om[j] >> (m & 63u)) & 1ull) != 0;
+      }
+#pragma unroll
+    for (uint32_t j = 0; j < SP; j++) nv += (uint32_t)__builtin_popcountll(vm[j]);
     uint32_t a = okm ? m + 1 : m;  // (the first mismatch's start is exact: its own size ends the step)
-    const uint32_t nv = (uint32_t)__builtin_popcountll(vma) + (uint32_t)__builtin_popcountll(vmb);
     if (a > nv) a = nv;
     if (a == 0) break;
-    if (lane < a) {
-      const uint32_t ps = pa + hla;
-      L.fl[n + lane] = fent{pa, ps, ps + pla, rotr8(kya, 0u - ps)};
-    }
-    if (64 + lane < a) {
-      const uint32_t ps = pb + hlb;
-      L.fl[n + 64 + lane] = fent{pb, ps, ps + plb, rotr8(kyb, 0u - ps)};
-    }
+#pragma unroll
+    for (uint32_t j = 0; j < SP; j++)
+      if (64u * j + lane < a) {
+        const uint32_t ps = pj[j] + hl[j];
+        L.fl[n + 64u * j + lane] = fent{pj[j], ps, ps + pl[j], rotr8(ky[j], 0u - ps)};
+      }
     // the last accepted frame is the chain state
-    const uint32_t l = a - 1, ll = l & 63u;
-    const bool inb = l >= 64;
-    const uint32_t lp = __builtin_amdgcn_readlane(inb ? pb : pa, ll);
-    const uint32_t lhl = __builtin_amdgcn_readlane(inb ? hlb : hla, ll);
-    const uint32_t lpl = __builtin_amdgcn_readlane(inb ? plb : pla, ll);
-    const uint32_t lkey = __builtin_amdgcn_readlane(inb ? kyb : kya, ll);
+    const uint32_t l = a - 1, ll = l & 63u, jl = l >> 6;
+    uint32_t lp = 0, lhl = 0, lpl = 0, lkey = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < SP; j++)
+      if (jl == j) {
+        lp = __builtin_amdgcn_readlane(pj[j], ll);
+        lhl = __builtin_amdgcn_readlane(hl[j], ll);
+        lpl = __builtin_amdgcn_readlane(pl[j], ll);
+        lkey = __builtin_amdgcn_readlane(ky[j], ll);
+      }
     S.cov_start = ss + lp;
     S.cov_ps = ss + lp + lhl;
     S.X = ss + lp + lhl + lpl;
@@ -1565,6 +1582,7 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          if (st_on && tid == 0) stat_add(P, ST_T_STRIDE, __builtin_amdgcn_s_memtime() - t_r0);
         }
         if (tid == 0 && !dense) chase_pass(P, L, ss, lo_c, k0);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1586,7 +1604,7 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
       // earlier stores drain before this segment's stores go out (measured
       // ~0.6 % faster on c3 than letting them overlap); the dense pass never
       // waits here (its chase is what the prefetch hides).
-      if (!dense) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!dense && !(P.opts & XYWS_OPT_RUNS_NOWAIT)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       XYWS_STAMP(acc_sync);
       const uint32_t nfl = L.nfl, hi_c = L.pass_hi;
@@ -1977,6 +1995,36 @@ XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32
     // (HBM would idle during the scan otherwise; the few header reads from
     // memory below and the publish's vmcnt(0) wait for them)
     if (ss + G::SEG < P.hi && !(P.opts & XYWS_OPT_DIAG)) io.issue(P, ss + G::SEG, tid);
+    // Lattice entry: when the previous call's frames were all F bytes long
+    // (P.pfs), the first frame start at or after rb on the lattice X0 + kF (X0:
+    // the batch's first frame start, after the carried frame) is tried first:
+    // it wins when its header opens a frame of exactly F bytes and its chain
+    // is plausible (the scan's own test). A speculation like the scan's
+    // winner: the predecessor's exact chain checks it at the hand-over.
+    if (P.pfs && ss == rb) {
+      if (tid == 0) {
+        const xyws_carry* cz = P.cin_user ? P.cin_user : &k_zero_carry;
+        uint64_t c0;
+        const cstate S0 = initial_state(P, cz, c0);
+        const uint64_t F = P.pfs, x0 = S0.X;
+        if (!(S0.st & (S_PARTIAL | S_PARTCARRY)) && x0 < P.hi) {
+          const uint64_t q = rb <= x0 ? x0 : x0 + (rb - x0 + F - 1) / F * F;
+          if (q >= ss && q + XYWS_MAX_FRAME_HEADER_SIZE <= ss + G::SEG && q < re) {
+            const hdr_info h = hdr_at(P, L, ss, q, NONE);
+            if (h.hlen && (uint64_t)h.hlen + h.plen == F && chain_plausible(P, L, ss, q, unm, false) == 1u)
+              L.best = (uint32_t)(q - ss);
+          }
+        }
+      }
+      __syncthreads();
+      if (L.best != 0xFFFFFFFFu) {
+        if (tid == 0) {
+          L.aux0 = ss + L.best;
+          stat_add(P, ST_P_LATTICE, 1);
+        }
+        break;
+      }
+    }
     scan_segment<G>(P, L, ss, tid, unm);
     if (stats_on(P) && tid == 0) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -2701,7 +2749,7 @@ __device__ __attribute__((always_inline)) inline void finish_call(run_params P, 
       st_store(hw + HW_EMIT_FLAG, (walked || st_load(hw + HW_EMIT_SLOW)) ? 1u : 0u);
       st_store(hw + HW_EMIT_SLOW, 0);
     }
-    pol_publish(P, L.E, 0);
+    pol_publish(P, L.E, G::NT == 512 ? 2u : 0u);  // (2: the run decoder in 512-thread workgroups)
     st_store(hw + HW_BAD, 0);
     st_store(hw + HW_TOTAL, 0);
     st_store(hw + HW_DONE, 0);
@@ -4221,6 +4269,18 @@ static bool sweep_preferred(const stream_scratch* s, uint64_t len) {
   const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
   return fsmax && fsmin == fsmax && fsmin >= SWEEP_MIN_FRAME;
 }
+// The run decoder's geometry, by the same statistics: regular frames under
+// WG512_MAX_FRAME take two 512-thread workgroups per CU on 64 KiB segments
+// (while one workgroup chases its segment, the other's stores drain: c2's
+// 264-byte frames 0.247 -> 0.181 ms, same box), the rest one 1024-thread
+// workgroup on 128 KiB segments (c1's 4 KiB frames 0.152 vs 0.158 ms; c4's
+// mixed sizes up to 1 MiB 0.496 vs 1.19).
+constexpr uint64_t WG512_MAX_FRAME = 2048;
+static bool wg512_preferred(const stream_scratch* s) {
+  if (!s->pol_h) return false;
+  const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
+  return fsmax && fsmin == fsmax && fsmax < WG512_MAX_FRAME;
+}
 
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
                         const xyws_carry* cin, xyws_carry* cout, xyws_frame* frames, uint64_t cap,
@@ -4237,7 +4297,8 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   // choice gives it (sweep_preferred), with no descriptors and none of the
   // run decoder's own modes.
   constexpr uint32_t RUN_MODES = XYWS_OPT_PARSE_ONLY | XYWS_OPT_WG512 | XYWS_OPT_DIAG | XYWS_OPT_TEST_GIVEUP |
-                                 XYWS_OPT_STEAL | XYWS_OPT_TEST_STEAL | XYWS_OPT_RUNS;
+                                 XYWS_OPT_STEAL | XYWS_OPT_TEST_STEAL | XYWS_OPT_RUNS | XYWS_OPT_NO_LATTICE |
+                                 XYWS_OPT_RUNS_NOWAIT | XYWS_OPT_WG1024 | XYWS_OPT_NO_LATENTRY;
   const bool want_sweep = (opts & XYWS_OPT_SWEEP) || (!small && sweep_preferred(s, hi - lo));
   if (want_sweep && !(frames && cap) && !(opts & RUN_MODES)) {
     const uint64_t seg = small ? G_SWEEP_SMALL::SEG : G_SWEEP::SEG;
@@ -4250,6 +4311,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     uint8_t* m = static_cast<uint8_t*>(s->mem);
     uint8_t* sm = static_cast<uint8_t*>(s->smem);
     run_params P;
+    P.pfs = 0;
     memset(&P, 0, sizeof(P));
     P.base = base; P.lo = lo; P.hi = hi;
     P.cout = cout; P.frames = nullptr; P.cap = 0; P.nframes = nframes;
@@ -4267,7 +4329,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     const uint32_t grid = (uint32_t)(nseg < maxg ? nseg : maxg);
     return small ? launch_sweep<G_SWEEP_SMALL>(P, grid, stream) : launch_sweep<G_SWEEP>(P, grid, stream);
   }
-  const bool wg512 = !small && (opts & XYWS_OPT_WG512) != 0;
+  const bool wg512 = !small && !(opts & XYWS_OPT_WG1024) && ((opts & XYWS_OPT_WG512) || wg512_preferred(s));
   const uint64_t seg = small ? G_SMALL::SEG : wg512 ? G_PROD2::SEG : G_PROD::SEG;
   // Runs get equal byte ranges (multiples of 16, one segment at least): every
   // workgroup streams the same number of bytes, and a run whose chain crosses
@@ -4310,6 +4372,13 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   P.cin = reinterpret_cast<xyws_carry*>(m + 64);
   P.fst = nullptr; P.rcap = 0;
   P.pol = s->pol_d;
+  // the lattice entry (find_entry): the previous call's frames all F bytes
+  // long, several per segment
+  P.pfs = 0;
+  if (s->pol_h && !(opts & XYWS_OPT_NO_LATENTRY)) {
+    const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
+    if (fsmax && fsmin == fsmax && fsmax <= seg / 4) P.pfs = fsmax;
+  }
   if (frames && cap) {
     const uint64_t rc_n = region_entries(cap, nruns);
     const int rc = fmem_grow(s, 8 * (uint64_t)P.nflat * rc_n, cs != hipStreamCaptureStatusNone);
