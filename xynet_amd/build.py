@@ -54,10 +54,11 @@ def build(force=False, verbose=False, extra=None):
     return [os.path.join(PKG, n) for n in TARGETS]
 
 
-# C++ callers of the header-only shim (include/xyws/websocket.hpp), run by the
-# GPU tests: linked against the in-tree libxyws.so (rpath), built here so the
+# C++ callers of the header-only shim (include/xyws/websocket.hpp) and of the
+# C-ABI (the loopback echo harness), run by the GPU tests: linked against the in-tree libxyws.so (rpath), built here so the
 # binary travels to the GPU box with the tree.
-CPP_TESTS = {"tests/cpp/test_shim": "tests/cpp/test_shim.cpp", "tests/cpp/test_compat": "tests/cpp/test_compat.cpp"}
+CPP_TESTS = {"tests/cpp/test_shim": "tests/cpp/test_shim.cpp", "tests/cpp/test_compat": "tests/cpp/test_compat.cpp",
+             "examples/echo_loopback": "examples/echo_loopback.cpp"}
 
 
 def build_cpp_tests(hipcc, force=False, verbose=False):

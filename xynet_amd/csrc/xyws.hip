@@ -572,33 +572,43 @@ int xyws_decode_stream(xyws_ctx* ctx, void* dev_buf, uint64_t len, const xyws_ca
 // machine has parsed so far (:305-385): flags from the first byte (FIN, opcode),
 // HAS_MASK and the 7-bit length from the second (0 for the 126/127 forms), the
 // extended length accumulated big-endian over the bytes received, the mask
-// bytes received so far; partial_result() computes that from the header bytes
-// fed since reset() (at most 13), which parse() keeps on the host.
+// bytes received so far; k_parser_partial computes that on the device from the
+// header bytes the decoder's carry holds (at most 13).
 struct xyws_parser {
   xyws_ctx* ctx;
   uint8_t* dev;       // device: carry (64 B) | frame (32 B) | count (8 B) | staging (32 B)
-  uint8_t* host;      // pinned: frame (32 B) | count (8 B) | input header bytes (16 B at +48)
+  uint8_t* host;      // pinned: frame (32 B) | count (8 B)
   uint64_t fed;       // header bytes fed since reset()
-  uint8_t hb[XYWS_MAX_FRAME_HEADER_SIZE];  // those bytes
   bool finished;
   xyws_frame res;
 };
 
-static void partial_result(const uint8_t* hb, uint64_t k, xyws_frame* r) {
-  memset(r, 0, sizeof *r);  // reset(): no flags, zero mask, zero length
-  if (k == 0) return;
-  r->flags = (uint8_t)((hb[0] & 0x0Fu) | ((hb[0] & 0x80u) ? XYWS_FLAG_FIN : 0u));
-  if (k == 1) return;
-  uint64_t len = hb[1] & 0x7Fu;
-  if (hb[1] & 0x80u) r->flags |= XYWS_FLAG_HAS_MASK;
-  const uint64_t ext = len == 127 ? 8 : len == 126 ? 2 : 0;
-  if (ext) {
-    len = 0;
-    for (uint64_t i = 2; i < 2 + ext && i < k; i++) len = (len << 8) | hb[i];
+// The parser's result() after an incomplete header, on the device from the
+// decoder's carry (the header bytes fed since reset(), hdr_len <= 13), as the
+// reference's state machine leaves it mid-header (websocket_frame_header.h:
+// 305-385: flags after byte 0, HAS_MASK and the 7-bit length after byte 1,
+// the 16/64-bit length accumulated byte by byte, the mask bytes so far).
+// Runs only when the decode completed no header (*count == 0).
+__global__ void k_parser_partial(const xyws_carry* __restrict__ carry, const uint64_t* __restrict__ count,
+                                 xyws_frame* __restrict__ r) {
+  if (threadIdx.x != 0 || *count != 0) return;
+  const uint8_t* hb = carry->hdr;
+  const unsigned k = carry->hdr_len;
+  xyws_frame f = {};  // reset(): no flags, zero mask, zero length
+  if (k >= 1) f.flags = (uint8_t)((hb[0] & 0x0Fu) | ((hb[0] & 0x80u) ? XYWS_FLAG_FIN : 0u));
+  if (k >= 2) {
+    uint64_t len = hb[1] & 0x7Fu;
+    if (hb[1] & 0x80u) f.flags |= XYWS_FLAG_HAS_MASK;
+    const unsigned ext = len == 127 ? 8 : len == 126 ? 2 : 0;
+    if (ext) {
+      len = 0;
+      for (unsigned i = 2; i < 2 + ext && i < k; i++) len = (len << 8) | hb[i];
+    }
+    f.payload_len = len;
+    if (f.flags & XYWS_FLAG_HAS_MASK)
+      for (unsigned i = 2 + ext; i < k && i < 2 + ext + 4; i++) f.key[i - 2 - ext] = hb[i];
   }
-  r->payload_len = len;
-  if (r->flags & XYWS_FLAG_HAS_MASK)
-    for (uint64_t i = 2 + ext; i < k && i < 2 + ext + 4; i++) r->key[i - 2 - ext] = hb[i];
+  *r = f;
 }
 
 int xyws_parser_create(xyws_ctx* ctx, xyws_parser** out) {
@@ -664,24 +674,21 @@ int xyws_parser_parse(xyws_parser* p, const void* data, uint64_t len, uint64_t* 
   if (!on_dev) {
     if (hipMemcpyAsync(stage, data, n, hipMemcpyHostToDevice, s) != hipSuccess) return XYWS_ERR_HIP;
     src = stage;
-    memcpy(p->hb + p->fed, data, n);
-  } else if (hipMemcpyAsync(p->host + 48, data, n, hipMemcpyDeviceToHost, s) != hipSuccess) {
-    return XYWS_ERR_HIP;
   }
   int rc = xyws_decode_stream(p->ctx, const_cast<void*>(src), n, carry, carry, frame, 1, count,
                               XYWS_OPT_PARSE_ONLY, stream);
   if (rc) return rc;
+  hipLaunchKernelGGL(k_parser_partial, dim3(1), dim3(64), 0, s, carry, count, frame);
+  if (hipGetLastError() != hipSuccess) return XYWS_ERR_HIP;
   if (hipMemcpyAsync(p->host, frame, 40, hipMemcpyDeviceToHost, s) != hipSuccess) return XYWS_ERR_HIP;
   if (hipStreamSynchronize(s) != hipSuccess) return XYWS_ERR_HIP;
   uint64_t nf;
   memcpy(&nf, p->host + 32, 8);
-  if (on_dev) memcpy(p->hb + p->fed, p->host + 48, n);
+  memcpy(&p->res, p->host, sizeof p->res);  // the header, or the partial state (k_parser_partial)
   if (nf == 0) {
     p->fed += n;
-    partial_result(p->hb, p->fed, &p->res);
     return XYWS_OK;
   }
-  memcpy(&p->res, p->host, sizeof p->res);
   p->finished = true;
   *consumed = p->res.hdr_len - p->fed;
   return XYWS_OK;
