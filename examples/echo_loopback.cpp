@@ -27,7 +27,7 @@
 // send. One JSON line on stdout; exit status 0 only when the bytes match.
 //
 //   echo_loopback [--frames N] [--max-len L] [--chunk B] [--ping-every K]
-//                 [--oversize] [--seed S] [--buf BYTES]
+//                 [--oversize] [--seed S] [--buf BYTES] [--opts DECODE_OPTS]
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -52,7 +52,8 @@
 namespace {
 
 struct opts_t {
-  uint64_t frames = 20000, max_len = 1000, chunk = 64 << 10, ping_every = 0, seed = 0x5EED0001, buf = 4 << 20;
+  uint64_t frames = 20000, max_len = 1000, chunk = 64 << 10, ping_every = 0, seed = 0x5EED0001, buf = 4 << 20,
+           opts = 0;
   bool oversize = false;
 };
 
@@ -118,7 +119,7 @@ struct server_stats {
 };
 
 // One connection, the GPU pipeline per recv batch.
-void serve(int fd, uint64_t B, server_stats& st) {
+void serve(int fd, uint64_t B, uint32_t opts, server_stats& st) {
   xyws_ctx* ctx = nullptr;
   XYCHK(xyws_ctx_create(0, &ctx));
   const uint64_t cap = B / 6 + 2;  // a masked frame is >= 6 bytes
@@ -134,10 +135,13 @@ void serve(int fd, uint64_t B, server_stats& st) {
   xyws_verdict* dverd;
   xyws_carry* dcarry;
   uint64_t* dsc;  // [0] nframes, [1] first_close, [2] out_len
+  uint64_t *doffs, *hoffs;  // reply offsets (cap + 1)
   HIPCHK(hipMalloc((void**)&dframes, cap * sizeof(xyws_frame)));
   HIPCHK(hipMalloc((void**)&dverd, cap * sizeof(xyws_verdict)));
   HIPCHK(hipMalloc((void**)&dcarry, sizeof(xyws_carry)));
   HIPCHK(hipMalloc((void**)&dsc, 4 * sizeof(uint64_t)));
+  HIPCHK(hipMalloc((void**)&doffs, (cap + 1) * sizeof(uint64_t)));
+  HIPCHK(hipHostMalloc((void**)&hoffs, (cap + 1) * sizeof(uint64_t)));
   struct small_t { uint64_t sc[4]; xyws_carry carry; xyws_frame last; xyws_verdict v; } *hs;
   HIPCHK(hipHostMalloc((void**)&hs, sizeof(small_t)));
 
@@ -152,40 +156,40 @@ void serve(int fd, uint64_t B, server_stats& st) {
       filled += (uint64_t)k;
     }
     HIPCHK(hipMemcpyAsync(din, hin, filled, hipMemcpyHostToDevice, s));
-    XYCHK(xyws_decode_stream(ctx, din, filled, nullptr, dcarry, dframes, cap, dsc, 0, s));
+    XYCHK(xyws_decode_stream(ctx, din, filled, nullptr, dcarry, dframes, cap, dsc, opts, s));
     HIPCHK(hipMemcpyAsync(hs->sc, dsc, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&hs->carry, dcarry, sizeof(xyws_carry), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     uint64_t nfr = hs->sc[0];
     if (nfr > cap) die("frame table overflow", (long)nfr);
-    uint64_t tail = filled - hs->carry.hdr_len, complete = nfr;
-    if (hs->carry.payload_remaining) {  // the last frame's payload continues past the batch
+    uint64_t complete = nfr;
+    const bool cut = hs->carry.payload_remaining != 0;  // the last frame's payload continues past the batch
+    if (cut) {
       complete = nfr - 1;
       HIPCHK(hipMemcpyAsync(&hs->last, dframes + complete, sizeof(xyws_frame), hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-      tail = (uint64_t)hs->last.frame_off;
+      if (!complete) HIPCHK(hipStreamSynchronize(s));  // (else read after the batch's next sync)
     }
     bool closing = false;
     if (complete) {
+      // one more round trip for the batch: classify, encode every complete
+      // frame (offsets per reply), copy back the replies (a server reply is
+      // never longer than the client frame it answers: <= filled bytes), the
+      // offsets and the first close index; the replies up to that index go out
       st.batches++;
       st.frames += complete;
       if (complete > st.max_batch) st.max_batch = complete;
       XYCHK(xyws_classify_frames(ctx, din, filled, dframes, complete, nullptr, 1000, 0, dverd, dsc + 1, s));
-      HIPCHK(hipMemcpyAsync(&hs->sc[1], dsc + 1, 8, hipMemcpyDeviceToHost, s));
+      XYCHK(xyws_encode_frames(ctx, din, filled, dframes, complete, nullptr, 0, XYWS_ENC_FRAME_OPCODE, nullptr,
+                               dverd, (1u << XYWS_ACT_DATA) | (1u << XYWS_ACT_PING), dout, B + 16, doffs, dsc + 2,
+                               s));
+      HIPCHK(hipMemcpyAsync(&hs->sc[1], dsc + 1, 16, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(hoffs, doffs, (complete + 1) * 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(hout, dout, filled, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
-      uint64_t first_close = hs->sc[1], reply_n = first_close < complete ? first_close : complete;
-      if (reply_n) {
-        XYCHK(xyws_encode_frames(ctx, din, filled, dframes, reply_n, nullptr, 0, XYWS_ENC_FRAME_OPCODE, nullptr,
-                                 dverd, (1u << XYWS_ACT_DATA) | (1u << XYWS_ACT_PING), dout, B + 16, nullptr,
-                                 dsc + 2, s));
-        HIPCHK(hipMemcpyAsync(&hs->sc[2], dsc + 2, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        uint64_t out_len = hs->sc[2];
-        if (out_len > B + 16) die("reply overflow", (long)out_len);
-        HIPCHK(hipMemcpyAsync(hout, dout, out_len, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        send_all(fd, hout, out_len);
-      }
+      const uint64_t first_close = hs->sc[1], out_len = hs->sc[2];
+      if (out_len > filled) die("reply longer than the batch", (long)out_len);
+      const uint64_t reply_len = first_close < complete ? hoffs[first_close] : out_len;
+      if (reply_len) send_all(fd, hout, reply_len);
       if (first_close < complete) {
         HIPCHK(hipMemcpyAsync(&hs->v, dverd + first_close, sizeof(xyws_verdict), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -196,6 +200,7 @@ void serve(int fd, uint64_t B, server_stats& st) {
       }
     }
     if (closing) break;
+    const uint64_t tail = cut ? (uint64_t)hs->last.frame_off : filled - hs->carry.hdr_len;
     std::memmove(hin, hin + tail, filled - tail);
     filled -= tail;
     if (filled == B) die("a frame larger than the receive buffer");
@@ -204,8 +209,8 @@ void serve(int fd, uint64_t B, server_stats& st) {
   xyws_ctx_last_device_error(ctx, &derr);
   if (derr) die("device error word", (long)derr);
   ::shutdown(fd, SHUT_WR);
-  hipHostFree(hin); hipHostFree(hout); hipHostFree(hs);
-  hipFree(din); hipFree(dout); hipFree(dframes); hipFree(dverd); hipFree(dcarry); hipFree(dsc);
+  hipHostFree(hin); hipHostFree(hout); hipHostFree(hs); hipHostFree(hoffs);
+  hipFree(doffs); hipFree(din); hipFree(dout); hipFree(dframes); hipFree(dverd); hipFree(dcarry); hipFree(dsc);
   hipStreamDestroy(s);
   xyws_ctx_destroy(ctx);
 }
@@ -223,6 +228,7 @@ int main(int argc, char** argv) {
     else if (a == "--ping-every") o.ping_every = num();
     else if (a == "--seed") o.seed = num();
     else if (a == "--buf") o.buf = num();
+    else if (a == "--opts") o.opts = num();  // xyws_decode_stream opts (experiments)
     else if (a == "--oversize") o.oversize = true;
     else die(("unknown option " + a).c_str());
   }
@@ -259,7 +265,7 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> got;
   got.reserve(expect.size() + 65536);
   auto t0 = std::chrono::steady_clock::now();
-  std::thread server([&] { serve(ss, o.buf, st); });
+  std::thread server([&] { serve(ss, o.buf, (uint32_t)o.opts, st); });
   std::thread receiver([&] {
     std::vector<uint8_t> b(1 << 20);
     for (;;) {
