@@ -498,3 +498,50 @@ def test_work_stealing_takes_pieces(ws, oracle, name, small):
     assert dec.ctx.last_device_error() == 0
     del buf, r
     torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size", [256 << 10, 1 << 20, 4 << 20, 24 << 20])
+def test_dense_first_segment_after_mixed_small_frames(ws, oracle, size):
+    """The run decoder's dense0 hint: after a call whose frames were small and
+    of mixed sizes, every run's first segment goes to the dense pass at once
+    (echo-sized batches: one segment per run). Calls on one stream: mixed
+    0-1000 B frames (sets the hint), the same again with descriptors and
+    without, then a batch whose payloads are themselves streams of valid
+    small frames (the dense pass's speculated entries land on fake headers
+    and are checked against the exact chain), then 64 KiB frames (the hint
+    off again). GPU vs oracle: bytes, count, descriptors, carry."""
+    rng = streams.SplitMix(0xDE45 + size)
+
+    pool, starts = bytearray(), []  # valid small frames, cut at frame starts into payloads
+    while len(pool) < (1 << 20):
+        starts.append(len(pool))
+        pool += streams.frame(rng, 0x81, rng.next() % 120)
+
+    def mixed(fake=False):
+        b = bytearray()
+        while len(b) < size:
+            n = rng.next() % 1001
+            if fake:
+                o = starts[rng.next() % (len(starts) - 64)]
+                inner = bytes(pool[o:o + n])
+                b += streams.header(0x82, len(inner), k := rng.bytes(4)) + streams.masked(inner, k)
+            else:
+                b += streams.frame(rng, 0x81, n)
+        return bytes(b[:size - 7])  # (ends inside a frame: the carry)
+    big = bytearray()
+    while len(big) < size:
+        big += streams.frame(rng, 0x82, 65536)
+    for src, desc in ((mixed(), True), (mixed(), True), (mixed(), False), (mixed(True), True),
+                      (bytes(big[:size]), True)):
+        dec = ws.frame_decoder()
+        view, _ = dev_bytes(src)
+        ob = np.frombuffer(src, np.uint8).copy()
+        ofr, carry, on = oracle.decode_stream(ob, cap=len(src) // 6 + 2)
+        r = dec.decode(view, cap=on + 2 if desc else 0)
+        assert r.nframes == on
+        assert host(view) == ob.tobytes()
+        if desc:
+            assert frames_list(r.frames(), True) == frames_list(ofr, True)
+        assert carry_list(dec.carry()) == carry_list(carry)
+        assert dec.ctx.last_device_error() == 0

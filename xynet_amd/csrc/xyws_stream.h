@@ -40,6 +40,8 @@ int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_ru
 #define XYWS_OPT_STATS 0x100u      // count speculation/repair events (xyws_debug_stats)
 #define XYWS_OPT_SMALL_SEG 0x200u  // 1 KiB segments, one per run: exercises run-boundary
                                    // speculation and repair on small test inputs
+#define XYWS_OPT_NO_DENSE0 0x1000u  // experiment (run decoder): the stride pass first in every run's first
+                                   // segment even after a call of small mixed-size frames (no dense0 hint)
 #define XYWS_OPT_NO_LATENTRY 0x4000u // experiment (run decoder): no lattice entry (find_entry scans every run)
 #define XYWS_OPT_WG1024 0x8000u    // the run decoder in its default geometry (one 1024-thread workgroup per CU),
                                    // whatever the geometry choice (wg512_preferred) would take

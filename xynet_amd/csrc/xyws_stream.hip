@@ -242,6 +242,8 @@ struct run_params {
   const xyws_carry* cin_user;  // caller's incoming carry (nullable; may alias cout)
   uint64_t pfs;                // run decoder: the frame size the previous call's frames all had (0: none;
                                // find_entry's lattice entry)
+  uint32_t dense0;             // run decoder: the previous call's frames were small and of mixed sizes:
+                               // a run's first segment goes to the dense pass at once (no stride try)
   xyws_carry* cin;        // private snapshot of it, written by run 0 (finish/emit read it)
   xyws_carry* cout;
   xyws_frame* frames;
@@ -2291,7 +2293,11 @@ XYWS_DEV void decode_range(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint
   if (tid == 0) {
     L.tail = 0; L.past = 0; L.ok = 0; L.done = 0; L.end = 0; L.tmo = 0; L.first_after = NONE;
     L.known = 0;
-    L.sgood = 1;
+    // (the stride pass first, unless the previous call's frames were small and
+    // irregular: a run of one or two segments would otherwise chase its first
+    // segment serially -- one LDS round trip per frame -- before the dense
+    // pass takes over from the second)
+    L.sgood = P.dense0 ? 0u : 1u;
     L.rng_end = rng_end;
     L.victim = victim ? 1u : 0u;
     L.hn = NONE; L.Wn = NONE; L.succ = P.nflat;
@@ -4275,11 +4281,17 @@ static bool sweep_preferred(const stream_scratch* s, uint64_t len) {
 // 264-byte frames 0.247 -> 0.181 ms, same box), the rest one 1024-thread
 // workgroup on 128 KiB segments (c1's 4 KiB frames 0.152 vs 0.158 ms; c4's
 // mixed sizes up to 1 MiB 0.496 vs 1.19).
+// Small frames of mixed sizes take it too when the batch is small (under one
+// 128 KiB segment per CU: the default geometry would give each run one
+// segment, and a run's latency is the call's): echo-sized batches of 0-1000 B
+// frames 115-135 -> 72-79 us per call (profiles/r03z_echo_geometry.txt).
 constexpr uint64_t WG512_MAX_FRAME = 2048;
-static bool wg512_preferred(const stream_scratch* s) {
+constexpr uint64_t DENSE0_MAX_FRAME = 2048;
+static bool wg512_preferred(const stream_scratch* s, uint64_t len) {
   if (!s->pol_h) return false;
   const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
-  return fsmax && fsmin == fsmax && fsmax < WG512_MAX_FRAME;
+  const bool small_batch = len < (uint64_t)s->ncu * G_PROD::SEG;
+  return fsmax && fsmax < WG512_MAX_FRAME && (fsmin == fsmax || small_batch);
 }
 
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
@@ -4329,7 +4341,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     const uint32_t grid = (uint32_t)(nseg < maxg ? nseg : maxg);
     return small ? launch_sweep<G_SWEEP_SMALL>(P, grid, stream) : launch_sweep<G_SWEEP>(P, grid, stream);
   }
-  const bool wg512 = !small && !(opts & XYWS_OPT_WG1024) && ((opts & XYWS_OPT_WG512) || wg512_preferred(s));
+  const bool wg512 = !small && !(opts & XYWS_OPT_WG1024) && ((opts & XYWS_OPT_WG512) || wg512_preferred(s, hi - lo));
   const uint64_t seg = small ? G_SMALL::SEG : wg512 ? G_PROD2::SEG : G_PROD::SEG;
   // Runs get equal byte ranges (multiples of 16, one segment at least): every
   // workgroup streams the same number of bytes, and a run whose chain crosses
@@ -4375,9 +4387,17 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   // the lattice entry (find_entry): the previous call's frames all F bytes
   // long, several per segment
   P.pfs = 0;
+  P.dense0 = 0;
   if (s->pol_h && !(opts & XYWS_OPT_NO_LATENTRY)) {
     const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
     if (fsmax && fsmin == fsmax && fsmax <= seg / 4) P.pfs = fsmax;
+  }
+  // small frames of mixed sizes last call (every run's last frame under
+  // DENSE0_MAX_FRAME, not all one size): the dense pass from each run's first
+  // segment (echo-sized batches of 0-1000 B frames: one segment per run)
+  if (s->pol_h && !(opts & XYWS_OPT_NO_DENSE0)) {
+    const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
+    if (fsmax && fsmin != fsmax && fsmax < DENSE0_MAX_FRAME) P.dense0 = 1;
   }
   if (frames && cap) {
     const uint64_t rc_n = region_entries(cap, nruns);
