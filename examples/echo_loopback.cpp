@@ -9,10 +9,19 @@
 //
 //   recv_some into a pinned buffer (as many bytes as the socket holds)
 //   -> H2D -> xyws_decode_stream (boundaries, unmask in place, frame table)
-//   -> xyws_classify_frames (max_payload 1000, the reference's checks)
-//   -> xyws_encode_frames (one reply per data frame: FIN + the frame's own
-//      opcode, unmasked server frame; pings answered as pongs)
+//   -> xyws_classify_frames (max_payload 1000, the reference's checks in its
+//      order, its bit-3 close test included: XYWS_POL_REFERENCE)
+//   -> xyws_encode_frames (one FIN|TEXT reply per data frame, unmasked server
+//      frame, as echo_once sends whatever the frame was)
 //   -> D2H of the replies -> send, then a close frame with the first close code.
+// The reference's test `flags & WS_OP_CLOSE` (websocket.h:87) is bit 3 of the
+// opcode, so it answers a ping (0x9), a pong (0xA) or opcodes 0xB-0xF with
+// close 1000; that is what this server does by default. `--rfc` departs from
+// the reference on purpose: pings get pongs carrying their payload, replies
+// keep the frame's own opcode, only a close frame closes 1000.
+// A header that announces more than 1000 payload bytes closes 1009 as soon as
+// the header is in (the reference checks before it receives the payload),
+// even when the frame's payload is still on its way.
 //
 // A frame cut by the recv boundary is kept (still masked) at the front of the
 // host buffer and decoded again with the next bytes, so every batch decodes
@@ -27,7 +36,8 @@
 // send. One JSON line on stdout; exit status 0 only when the bytes match.
 //
 //   echo_loopback [--frames N] [--max-len L] [--chunk B] [--ping-every K]
-//                 [--oversize] [--seed S] [--buf BYTES] [--opts DECODE_OPTS]
+//                 [--oversize] [--oversize-len L] [--seed S] [--buf BYTES]
+//                 [--opts DECODE_OPTS] [--rfc]
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -53,8 +63,8 @@ namespace {
 
 struct opts_t {
   uint64_t frames = 20000, max_len = 1000, chunk = 64 << 10, ping_every = 0, seed = 0x5EED0001, buf = 4 << 20,
-           opts = 0;
-  bool oversize = false;
+           opts = 0, oversize_len = 1001;
+  bool oversize = false, rfc = false;
 };
 
 [[noreturn]] void die(const char* what, long rc = 0) {
@@ -84,15 +94,19 @@ void append_frame(std::vector<uint8_t>& out, uint8_t flags, const uint8_t* key, 
     for (uint64_t i = 0; i < len; ++i) out[at + i] ^= key[i & 3];  // websocket_mask, phase 0
 }
 
-// The client's stream and the reply stream the reference's echo would send.
-void build_streams(const opts_t& o, std::vector<uint8_t>& wire, std::vector<uint8_t>& expect, uint64_t& payload) {
+// The client's stream and the reply stream the reference's echo would send
+// (or, with --rfc, an RFC 6455 server: pongs for pings).
+void build_streams(const opts_t& o, std::vector<uint8_t>& wire, std::vector<uint8_t>& expect, uint64_t& payload,
+                   uint64_t& echoes, uint16_t& code) {
   std::mt19937_64 rng(o.seed);
   std::vector<uint8_t> p;
   payload = 0;
+  echoes = 0;
+  code = 0;
   for (uint64_t i = 0; i < o.frames; ++i) {
     bool ping = o.ping_every && (i % o.ping_every) == o.ping_every - 1;
     uint64_t len = rng() % ((ping ? std::min<uint64_t>(o.max_len, 125) : o.max_len) + 1);
-    if (o.oversize && i == o.frames - 1) len = 1001;
+    if (o.oversize && i == o.frames - 1) len = o.oversize_len;
     p.resize(len);
     for (auto& b : p) b = (uint8_t)(0x20 + rng() % 95);
     uint8_t key[4];
@@ -100,12 +114,15 @@ void build_streams(const opts_t& o, std::vector<uint8_t>& wire, std::vector<uint
     std::memcpy(key, &k, 4);
     uint8_t op = ping ? XYWS_FLAG_OP_PING : XYWS_FLAG_OP_TEXT;
     append_frame(wire, op | XYWS_FLAG_FIN | XYWS_FLAG_HAS_MASK, key, p.data(), len);
-    if (len > 1000) break;  // the server closes with 1009 here
+    if (ping && !o.rfc && !code) code = 1000;  // the reference closes on a ping (websocket.h:87)
+    if (len > 1000 && !code) code = 1009;      // the server closes with 1009 here
+    if (code) break;                           // (the server has closed: the client stops here)
     append_frame(expect, (ping ? XYWS_FLAG_OP_PONG : XYWS_FLAG_OP_TEXT) | XYWS_FLAG_FIN, nullptr, p.data(), len);
     payload += len;
+    echoes++;
   }
-  uint16_t code = o.oversize ? 1009 : 1000;
-  if (!o.oversize) {
+  if (!code) {
+    code = 1000;
     uint8_t key[4] = {0x11, 0x22, 0x33, 0x44}, be[2] = {0x03, 0xE8};
     append_frame(wire, XYWS_FLAG_OP_CLOSE | XYWS_FLAG_FIN | XYWS_FLAG_HAS_MASK, key, be, 2);
   }
@@ -114,12 +131,12 @@ void build_streams(const opts_t& o, std::vector<uint8_t>& wire, std::vector<uint
 }
 
 struct server_stats {
-  uint64_t batches = 0, frames = 0, max_batch = 0;
+  uint64_t batches = 0, frames = 0, max_batch = 0, early_close = 0;
   uint16_t close_code = 0;
 };
 
 // One connection, the GPU pipeline per recv batch.
-void serve(int fd, uint64_t B, uint32_t opts, server_stats& st) {
+void serve(int fd, uint64_t B, uint32_t opts, bool rfc, server_stats& st) {
   xyws_ctx* ctx = nullptr;
   XYCHK(xyws_ctx_create(0, &ctx));
   const uint64_t cap = B / 6 + 2;  // a masked frame is >= 6 bytes
@@ -170,7 +187,11 @@ void serve(int fd, uint64_t B, uint32_t opts, server_stats& st) {
       if (!complete) HIPCHK(hipStreamSynchronize(s));  // (else read after the batch's next sync)
     }
     bool closing = false;
-    if (complete) {
+    // frames with a complete header: every complete frame, and the cut one
+    // (its header alone decides a close: the reference checks the header
+    // before it receives the payload, websocket.h:117-128)
+    const uint64_t nchk = nfr;
+    if (nchk) {
       // one more round trip for the batch: classify, encode every complete
       // frame (offsets per reply), copy back the replies (a server reply is
       // never longer than the client frame it answers: <= filled bytes), the
@@ -178,19 +199,26 @@ void serve(int fd, uint64_t B, uint32_t opts, server_stats& st) {
       st.batches++;
       st.frames += complete;
       if (complete > st.max_batch) st.max_batch = complete;
-      XYCHK(xyws_classify_frames(ctx, din, filled, dframes, complete, nullptr, 1000, 0, dverd, dsc + 1, s));
-      XYCHK(xyws_encode_frames(ctx, din, filled, dframes, complete, nullptr, 0, XYWS_ENC_FRAME_OPCODE, nullptr,
-                               dverd, (1u << XYWS_ACT_DATA) | (1u << XYWS_ACT_PING), dout, B + 16, doffs, dsc + 2,
-                               s));
+      const uint32_t policy = rfc ? 0u : XYWS_POL_REFERENCE;
+      XYCHK(xyws_classify_frames(ctx, din, filled, dframes, nchk, nullptr, 1000, policy, dverd, dsc + 1, s));
+      if (complete) {
+        const uint8_t flags = rfc ? 0 : (XYWS_FLAG_FIN | XYWS_FLAG_OP_TEXT);
+        const uint32_t acts = rfc ? (1u << XYWS_ACT_DATA) | (1u << XYWS_ACT_PING) : (1u << XYWS_ACT_DATA);
+        XYCHK(xyws_encode_frames(ctx, din, filled, dframes, complete, nullptr, flags, rfc ? XYWS_ENC_FRAME_OPCODE : 0,
+                                 nullptr, dverd, acts, dout, B + 16, doffs, dsc + 2, s));
+        HIPCHK(hipMemcpyAsync(hoffs, doffs, (complete + 1) * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(hout, dout, filled, hipMemcpyDeviceToHost, s));
+      } else {
+        HIPCHK(hipMemsetAsync(dsc + 2, 0, 8, s));
+      }
       HIPCHK(hipMemcpyAsync(&hs->sc[1], dsc + 1, 16, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipMemcpyAsync(hoffs, doffs, (complete + 1) * 8, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipMemcpyAsync(hout, dout, filled, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       const uint64_t first_close = hs->sc[1], out_len = hs->sc[2];
       if (out_len > filled) die("reply longer than the batch", (long)out_len);
       const uint64_t reply_len = first_close < complete ? hoffs[first_close] : out_len;
       if (reply_len) send_all(fd, hout, reply_len);
-      if (first_close < complete) {
+      if (first_close < nchk) {
+        if (first_close == complete) st.early_close = 1;  // (closed on the cut frame's header)
         HIPCHK(hipMemcpyAsync(&hs->v, dverd + first_close, sizeof(xyws_verdict), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         st.close_code = hs->v.close_code;
@@ -230,13 +258,18 @@ int main(int argc, char** argv) {
     else if (a == "--buf") o.buf = num();
     else if (a == "--opts") o.opts = num();  // xyws_decode_stream opts (experiments)
     else if (a == "--oversize") o.oversize = true;
+    else if (a == "--oversize-len") o.oversize_len = num();
+    else if (a == "--rfc") o.rfc = true;
     else die(("unknown option " + a).c_str());
   }
-  if (o.max_len > 1000 || o.frames == 0 || o.chunk == 0 || o.buf < 4096) die("bad options");
+  if (o.max_len > 1000 || o.frames == 0 || o.chunk == 0 || o.buf < 4096 || o.oversize_len <= 1000 ||
+      o.oversize_len > (32u << 20))
+    die("bad options");
 
   std::vector<uint8_t> wire, expect;
-  uint64_t payload = 0;
-  build_streams(o, wire, expect, payload);
+  uint64_t payload = 0, want_echoes = 0;
+  uint16_t want_code = 0;
+  build_streams(o, wire, expect, payload, want_echoes, want_code);
 
   int ls = ::socket(AF_INET, SOCK_STREAM, 0);
   sockaddr_in addr{};
@@ -265,7 +298,7 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> got;
   got.reserve(expect.size() + 65536);
   auto t0 = std::chrono::steady_clock::now();
-  std::thread server([&] { serve(ss, o.buf, (uint32_t)o.opts, st); });
+  std::thread server([&] { serve(ss, o.buf, (uint32_t)o.opts, o.rfc, st); });
   std::thread receiver([&] {
     std::vector<uint8_t> b(1 << 20);
     for (;;) {
@@ -281,16 +314,20 @@ int main(int argc, char** argv) {
   double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   ::close(cs); ::close(ss); ::close(ls);
 
-  bool ok = got == expect;
-  uint64_t echoed = st.frames - (st.close_code ? 1 : 0);
+  // (a close on a complete frame counts that frame in st.frames; one on a cut
+  // frame's header does not)
+  uint64_t echoed = st.frames - ((st.close_code && !st.early_close) ? 1 : 0);
+  bool ok = got == expect && st.close_code == want_code && echoed == want_echoes;
   std::printf("{\"harness\": \"echo_loopback\", \"ok\": %s, \"frames\": %lu, \"payload_bytes\": %lu, "
               "\"wire_bytes_in\": %zu, \"reply_bytes\": %zu, \"close_code\": %u, \"seconds\": %.6f, "
               "\"frames_per_s\": %.1f, \"payload_MBps\": %.2f, \"wire_in_MBps\": %.2f, \"batches\": %lu, "
-              "\"frames_per_batch_avg\": %.1f, \"frames_per_batch_max\": %lu, \"chunk\": %lu, \"max_len\": %lu}\n",
+              "\"frames_per_batch_avg\": %.1f, \"frames_per_batch_max\": %lu, \"chunk\": %lu, \"max_len\": %lu, "
+              "\"mode\": \"%s\", \"closed_on_header\": %s}\n",
               ok ? "true" : "false", (unsigned long)echoed, (unsigned long)payload, wire.size(), got.size(),
               st.close_code, sec, echoed / sec, payload / sec / 1e6, wire.size() / sec / 1e6,
               (unsigned long)st.batches, st.batches ? (double)st.frames / st.batches : 0.0,
-              (unsigned long)st.max_batch, (unsigned long)o.chunk, (unsigned long)o.max_len);
+              (unsigned long)st.max_batch, (unsigned long)o.chunk, (unsigned long)o.max_len,
+              o.rfc ? "rfc" : "reference", st.early_close ? "true" : "false");
   if (!ok) {
     size_t i = 0;
     while (i < got.size() && i < expect.size() && got[i] == expect[i]) ++i;

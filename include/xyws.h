@@ -147,9 +147,10 @@ int xyws_ctx_destroy(xyws_ctx* ctx);
 /* Pre-size scratch for batches up to `max_batch_bytes` (and, for indexed mode
  * and frame descriptors, `max_frames` frames) so that later calls allocate
  * nothing and can be captured into a hipGraph. The per-frame tables go to the
- * streams already used on the context, and to a new stream at its first
- * uncaptured call (make one before capturing on it). Calls on larger
- * batches grow scratch lazily. */
+ * streams already used on the context and to one spare: the first stream new
+ * to the context may be captured at once; a second new stream needs one
+ * uncaptured call first (or XYWS_ERR_CAPACITY). Calls on larger batches grow
+ * scratch lazily. */
 int xyws_ctx_reserve(xyws_ctx* ctx, uint64_t max_batch_bytes, uint64_t max_frames);
 /* Device-side error word of the last completed call (0 = none). Synchronizes
  * the context's device. */
@@ -172,6 +173,12 @@ int xyws_unmask(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4],
  * Not allowed during stream capture (XYWS_ERR_CAPACITY). */
 int xyws_mask_bytes(xyws_ctx* ctx, void* data, uint64_t len, const uint8_t key[4],
                     uint64_t phase, uint64_t* phase_out, void* stream);
+/* xyws_mask_bytes refuses device memory of another device than ctx's
+ * (XYWS_ERR_INVALID; xyws_unmask takes ctx's device memory only, unchecked:
+ * no pointer query on the hot path). xyws_pointer_device: *device = the HIP device whose
+ * memory `p` points into, or -1 for host memory (pinned, registered or
+ * pageable); the shim uses it to pick the per-device context. */
+int xyws_pointer_device(const void* p, int* device);
 
 /* Frames at caller-known offsets (ascending, non-overlapping) inside one
  * device buffer: parse each header as websocket_frame_header_parser::parse
@@ -269,6 +276,9 @@ int xyws_encode_frames(xyws_ctx* ctx, const void* dev_src, uint64_t src_len,
 #define XYWS_POL_UNMASKED   0x2u /* accept unmasked frames instead of closing 1008 */
 #define XYWS_POL_STRICT     0x4u /* RFC 6455 protocol errors (RSV, reserved opcode, fragmented or
                                     >125-byte control frame) close 1002 (the reference accepts them) */
+#define XYWS_POL_REFERENCE  0x8u /* the reference's own close test, bug included: `flags & WS_OP_CLOSE`
+                                    (websocket.h:87) is bit 3 of the opcode, so ping, pong and opcodes
+                                    0xB-0xF close 1000 like a close frame (echo_once answers nothing else) */
 struct xyws_verdict {
   uint16_t close_code; /* 0, or the code the connection closes with */
   uint16_t peer_code;  /* close frames: the peer's status code (1005 if none) */
@@ -329,7 +339,12 @@ int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len,
  * the submission completed. Submissions complete in order. A submission's
  * results stay valid until its slot is reused, which happens only after
  * poll() or wait() returned them: submit() returns XYWS_ERR_AGAIN while
- * XYWS_ARENA_SLOTS submissions are in flight or unclaimed. */
+ * XYWS_ARENA_SLOTS submissions are in flight or unclaimed. wait() blocks on
+ * that submission's own completion event, not on the shared stream (other
+ * connections' later work is not waited for). Arenas that share a stream
+ * share its scratch slot, so the decoder choice one arena's batches steer
+ * (which decoder, which geometry: speed only, never bytes) applies to the
+ * next batch of any arena on that stream. */
 #define XYWS_ARENA_SLOTS 8
 /* A submit that fails before anything was enqueued leaves the arena as it
  * was; one that fails later (the decode or a copy back could not be

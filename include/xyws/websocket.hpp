@@ -43,6 +43,7 @@
 #include <tuple>
 #include <type_traits>
 #include <utility>
+#include <vector>
 
 #include "../xyws.h"
 
@@ -153,35 +154,98 @@ inline std::size_t websocket_mask(context& ctx, std::span<std::byte> dev_data, s
   return static_cast<std::size_t>(out);
 }
 
-// The calling thread's context on device 0 (what default-constructed parsers
+// The calling thread's context on `device` (what default-constructed parsers
 // and the reference-signature websocket_mask use, so `websocket_frame_header_parser{}`
 // and `websocket_mask(data_span, mask, 0)` read as in the reference).
-inline context& default_context() {
-  thread_local context ctx(0);
-  return ctx;
+inline context& default_context(int device = 0) {
+  constexpr int MAXDEV = 64;
+  thread_local std::array<context*, MAXDEV> ctxs{};
+  if (device < 0 || device >= MAXDEV) device = 0;
+  if (!ctxs[device]) {
+    thread_local struct owner {
+      std::array<context*, MAXDEV>* v;
+      ~owner() {
+        for (auto* c : *v) delete c;
+      }
+    } own{&ctxs};
+    ctxs[device] = new context(device);
+  }
+  return *ctxs[device];
 }
 
-// websocket_mask(R&& data, uint32_t mask, size_t i) with the reference's
-// signature and contract (websocket_frame_mask.h:6-25): any contiguous range
-// of byte-sized elements, host or device memory, unmasked in place when it
-// returns; returns i + size. On the device through xyws_mask_bytes (host
-// bytes staged: a compatibility path; batches go through frame_decoder).
+namespace detail {
+// websocket_mask's element types (websocket_frame_mask.h:6-13): anything
+// convertible to std::byte, char or unsigned char
+template <typename T>
+inline constexpr bool mask_element_v = std::is_convertible_v<T, std::byte> || std::is_convertible_v<T, char> ||
+                                       std::is_convertible_v<T, unsigned char> || std::is_same_v<T, std::byte>;
+// a range the device can XOR where it lies: contiguous bytes
 template <typename R>
-  requires std::ranges::contiguous_range<R> && std::ranges::sized_range<R> &&
-           (sizeof(std::ranges::range_value_t<R>) == 1) &&
-           (std::is_convertible_v<std::ranges::range_value_t<R>, std::byte> ||
-            std::is_convertible_v<std::ranges::range_value_t<R>, char> ||
-            std::is_convertible_v<std::ranges::range_value_t<R>, unsigned char> ||
-            std::is_same_v<std::ranges::range_value_t<R>, std::byte>)
-std::size_t websocket_mask(R&& data, std::uint32_t mask, std::size_t i) {
+concept contiguous_bytes = std::ranges::contiguous_range<R> && std::ranges::sized_range<R> &&
+                           (sizeof(std::ranges::range_value_t<R>) == 1);
+// a range of such pieces behind a view (std::views::join over spans: the
+// reference's only multi-piece use, test/playground.cpp:188-189)
+template <typename R>
+concept joined_pieces = requires(R& r) {
+  { r.base() } -> std::ranges::range;
+} && contiguous_bytes<std::ranges::range_reference_t<decltype(std::declval<R&>().base())>>;
+
+// one contiguous piece (host or device bytes), on the device of its memory
+inline std::size_t mask_piece(void* p, std::size_t n, std::uint32_t mask, std::size_t i) {
+  if (n == 0) return i;
   const std::uint8_t key[4] = {std::uint8_t(mask), std::uint8_t(mask >> 8), std::uint8_t(mask >> 16),
                                std::uint8_t(mask >> 24)};
+  int dev = -1;
+  (void)xyws_pointer_device(p, &dev);
   std::uint64_t out = 0;
-  check(xyws_mask_bytes(default_context().native(), const_cast<void*>(static_cast<const void*>(std::ranges::data(data))),
-                        std::ranges::size(data), key, i, &out, nullptr),
+  check(xyws_mask_bytes(default_context(dev < 0 ? 0 : dev).native(), p, n, key, i, &out, nullptr),
         "xyws_mask_bytes");
   return static_cast<std::size_t>(out);
 }
+}  // namespace detail
+
+}  // namespace xyws
+
+// websocket_mask(R&& data, uint32_t mask, size_t i) with the reference's
+// signature, scope and contract (websocket_frame_mask.h:6-25, declared in the
+// global namespace there too): any range of byte-sized elements, host or
+// device memory, unmasked in place when it returns, data[j] ^= bytes(mask)[(i
+// + j) % 4]; returns i + the range's length. The XOR runs on the device
+// through xyws_mask_bytes (host bytes staged: a compatibility path; batches
+// go through xyws::frame_decoder):
+//  * a contiguous range: one call where it lies;
+//  * a view over contiguous pieces (std::views::join of spans, as
+//    test/playground.cpp:188-189 masks two joined spans): one call per piece,
+//    the phase carried from piece to piece;
+//  * any other range: its elements staged in one host buffer, one call,
+//    written back in order.
+template <typename R>
+  requires std::ranges::range<R> && xyws::detail::mask_element_v<std::ranges::range_value_t<R>>
+std::size_t websocket_mask(R&& data, std::uint32_t mask, std::size_t i) {
+  using namespace xyws::detail;
+  if constexpr (contiguous_bytes<R>) {
+    return mask_piece(const_cast<void*>(static_cast<const void*>(std::ranges::data(data))), std::ranges::size(data),
+                      mask, i);
+  } else if constexpr (joined_pieces<std::remove_reference_t<R>>) {
+    for (auto&& piece : data.base())
+      i = mask_piece(const_cast<void*>(static_cast<const void*>(std::ranges::data(piece))), std::ranges::size(piece),
+                     mask, i);
+    return i;
+  } else {
+    std::vector<unsigned char> stage;
+    for (auto&& c : data) stage.push_back(static_cast<unsigned char>(c));
+    const std::size_t r = mask_piece(stage.data(), stage.size(), mask, i);
+    std::size_t j = 0;
+    for (auto it = std::ranges::begin(data); it != std::ranges::end(data); ++it, ++j)
+      *it = static_cast<std::ranges::range_value_t<R>>(stage[j]);
+    return r;
+  }
+}
+
+namespace xyws {
+// (the same function under the shim's namespace: xyws::websocket_mask(data,
+// mask, i) and, through namespace xynet below, the reference's spelling)
+using ::websocket_mask;
 
 // A decoded frame (device descriptor copied to the host by the caller).
 struct frame : xyws_frame {

@@ -340,7 +340,8 @@ uint64_t oracle_encode_frames(const uint8_t* src, uint64_t src_len, const xyws_f
  * 1003, unmasked -> 1008, length > max -> 1009, first match wins; without its
  * bit-3 test (`flags & WS_OP_CLOSE` is also true for ping and pong). Policy
  * bits: XYWS_POL_FRAGMENTS skips the FIN test, XYWS_POL_UNMASKED the mask
- * test, XYWS_POL_STRICT puts RFC protocol errors (1002) first. *first: the
+ * test, XYWS_POL_STRICT puts RFC protocol errors (1002) first, XYWS_POL_REFERENCE
+ * restores the bit-3 test (websocket.h:87: ping, pong, 0xB-0xF close 1000). *first: the
  * first closing frame, or UINT64_MAX. */
 void oracle_classify(const uint8_t* src, uint64_t src_len, const xyws_frame* frames, uint64_t n,
                      uint64_t max_payload, uint32_t policy, xyws_verdict* out, uint64_t* first) {
@@ -354,7 +355,7 @@ void oracle_classify(const uint8_t* src, uint64_t src_len, const xyws_frame* fra
     int proto = (f->status & (XYWS_ST_RSV | XYWS_ST_RESERVED_OPCODE | XYWS_ST_BAD_CONTROL)) != 0;
     uint16_t code = 0;
     if ((policy & XYWS_POL_STRICT) && proto) code = 1002;
-    else if (op == XYWS_FLAG_OP_CLOSE) code = 1000;
+    else if (op == XYWS_FLAG_OP_CLOSE || ((policy & XYWS_POL_REFERENCE) && (op & 8u))) code = 1000;
     else if (!(f->flags & XYWS_FLAG_FIN) && !(policy & XYWS_POL_FRAGMENTS)) code = 1003;
     else if (!(f->flags & XYWS_FLAG_HAS_MASK) && !(policy & XYWS_POL_UNMASKED)) code = 1008;
     else if (f->payload_len > max_payload) code = 1009;

@@ -14,6 +14,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <deque>
 #include <vector>
 
 #include "xyws/websocket.hpp"  // was xynet/http/websocket_frame_header.h + websocket_frame_mask.h
@@ -135,6 +136,34 @@ int main(int argc, char** argv) {
     for (size_t j = 0; j < v.size(); j++)
       if (v[j] != (unsigned char)(key >> (8 * ((6 + j) % 4)))) { printf("FAIL phase byte %zu\n", j); return 1; }
     if (r != 43) { printf("FAIL return %zu\n", r); return 1; }
+    ok++;
+  }
+  // a non-contiguous range: two spans joined (test/playground.cpp:180-194,
+  // masked twice there; here once, then checked), the phase carried across
+  // the pieces; then a deque (staged through one host buffer)
+  {
+    uint32_t mask = 0x9d3c5a17u;
+    auto data1 = vector<char>{'g', 'g', 'g', 'x', 'y'};
+    auto data2 = array<char, 3>{'g', 'g', '2'};
+    const auto want1 = data1;
+    const auto want2 = data2;
+    auto span1 = std::span{data1.begin(), data1.size()};
+    auto span2 = std::span{data2.begin(), data2.size()};
+    auto join_data = std::array<std::span<char, std::dynamic_extent>, 2>{span1, span2};
+    auto i = websocket_mask(join_data | std::views::join, mask, 0);
+    const auto* kb = reinterpret_cast<const unsigned char*>(&mask);
+    for (size_t j = 0; j < 8; j++) {
+      const char got = j < 5 ? data1[j] : data2[j - 5];
+      const char was = j < 5 ? want1[j] : want2[j - 5];
+      if ((unsigned char)got != ((unsigned char)was ^ kb[j % 4])) { printf("FAIL joined byte %zu\n", j); return 1; }
+    }
+    if (i != 8) { printf("FAIL joined return %zu\n", i); return 1; }
+    ok++;
+    deque<unsigned char> dq(23, 0x5a);
+    const size_t r = websocket_mask(dq, mask, 3);
+    for (size_t j = 0; j < dq.size(); j++)
+      if (dq[j] != (0x5a ^ kb[(3 + j) % 4])) { printf("FAIL deque byte %zu\n", j); return 1; }
+    if (r != 26) { printf("FAIL deque return %zu\n", r); return 1; }
     ok++;
   }
   printf("ok %d\n", ok);

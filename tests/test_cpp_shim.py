@@ -116,4 +116,4 @@ def test_websocket_h_caller_on_device():
     assert os.path.exists(COMPAT_BIN), "tests/cpp/test_compat not built (run __graft_entry__.build())"
     r = subprocess.run([COMPAT_BIN], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "ok 33" in r.stdout, r.stdout
+    assert "ok 35" in r.stdout, r.stdout

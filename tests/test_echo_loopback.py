@@ -4,7 +4,10 @@ of example/include/common/websocket.h:81-108) over a real 127.0.0.1 TCP
 connection, decoding / classifying / encoding each recv batch on the GPU.
 The harness checks the whole reply stream byte for byte against the replies
 the reference's echo sends (FIN|TEXT echo per frame, a close frame with the
-first close code) and exits non-zero on any difference.
+first close code) and exits non-zero on any difference. By default the server
+is the reference's, its bit-3 close test included (websocket.h:87: a ping
+closes 1000); `--rfc` is an RFC 6455 server instead (pings answered with
+pongs), a deliberate departure from the reference tested on its own.
 """
 import json
 import os
@@ -37,9 +40,19 @@ def test_echo_replies_match_reference_echo(chunk):
 
 
 @pytest.mark.gpu
-def test_echo_pings_get_pongs():
+def test_echo_ping_closes_1000_like_the_reference():
+    # websocket.h:87 tests `flags & WS_OP_CLOSE`, bit 3 of the opcode: the
+    # reference's echo answers the first ping (0x9) with close 1000, and every
+    # frame before it with a FIN|TEXT echo
     j = run("--frames", 4000, "--ping-every", 7, "--chunk", 4096)
-    assert j["ok"] and j["close_code"] == 1000
+    assert j["ok"] and j["close_code"] == 1000 and j["frames"] == 6 and j["mode"] == "reference"
+
+
+@pytest.mark.gpu
+def test_echo_rfc_mode_pings_get_pongs():
+    # --rfc departs from the reference on purpose: pongs for pings
+    j = run("--frames", 4000, "--ping-every", 7, "--chunk", 4096, "--rfc")
+    assert j["ok"] and j["close_code"] == 1000 and j["mode"] == "rfc"
 
 
 @pytest.mark.gpu
@@ -47,6 +60,16 @@ def test_echo_pings_get_pongs():
 def test_echo_oversize_frame_closes_1009(chunk):
     j = run("--frames", 2000, "--oversize", "--chunk", chunk)
     assert j["ok"] and j["close_code"] == 1009 and j["frames"] == 1999
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [4096, 65536])
+def test_echo_oversize_header_closes_before_its_payload(chunk):
+    # a header announcing 200 000 B (far past the 4 KiB receive buffer): the
+    # reference closes 1009 on the header (websocket.h:102-105), before the
+    # payload arrives; the server must not wait for it
+    j = run("--frames", 500, "--oversize", "--oversize-len", 200000, "--buf", 4096, "--chunk", chunk)
+    assert j["ok"] and j["close_code"] == 1009 and j["frames"] == 499 and j["closed_on_header"]
 
 
 @pytest.mark.gpu

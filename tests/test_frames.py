@@ -76,6 +76,37 @@ def test_oracle_reassembly_matches_the_generator(oracle):
             assert bool(r.status & 2) == (not ok)
 
 
+def test_oracle_reference_policy_is_the_bit3_test(oracle):
+    """XYWS_POL_REFERENCE restates websocket_check_parser_result in its own
+    order (example/include/common/websocket.h:81-108): `flags & WS_OP_CLOSE`
+    (bit 3 of the opcode: close, ping, pong, 0xB-0xF) -> 1000, then FIN=0 ->
+    1003, unmasked -> 1008, length > max -> 1009."""
+    rng = streams.SplitMix(77)
+    ops = [0x81, 0x89, 0x8A, 0x8B, 0x88, 0x02, 0x82, 0x8F, 0x80]
+    wire = b"".join(streams.frame(rng, b0, 5) for b0 in ops) + streams.frame(rng, 0x81, 3, masked_frame=False) + \
+        streams.frame(rng, 0x82, 1001)
+    host = np.frombuffer(wire, np.uint8).copy()
+    frames, _, n = oracle.decode_stream(host)
+    verd, first = oracle.classify(host, frames, 1000, 8)
+    want = []
+    for f in frames:
+        fl = f.flags
+        if fl & 0x08:
+            want.append(1000)
+        elif not fl & 0x10:
+            want.append(1003)
+        elif not fl & 0x20:
+            want.append(1008)
+        elif f.payload_len > 1000:
+            want.append(1009)
+        else:
+            want.append(0)
+    assert [v.close_code for v in verd] == want
+    assert want[:3] == [0, 1000, 1000] and first == 1
+    verd0, _ = oracle.classify(host, frames, 1000, 0)
+    assert [v.close_code for v in verd0][:4] == [0, 0, 0, 0]  # without the bug: ping, pong, 0xB deliver
+
+
 def test_oracle_encode_headers_match_reference_builds(oracle):
     from conftest import load_golden
     g = load_golden("frame_header.json")
@@ -220,7 +251,7 @@ def test_encode_selected_by_verdicts_and_device_count(ws, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("policy", [0, 1, 2, 5, 7])
+@pytest.mark.parametrize("policy", [0, 1, 2, 5, 7, 8, 9])
 @pytest.mark.parametrize("case", ["msgs", "unmasked_mix", "rsv_reserved_ops", "bad_control", "closes"])
 def test_classify_vs_oracle(ws, oracle, policy, case):
     rng = streams.SplitMix(123)

@@ -364,13 +364,17 @@ int xyws_ctx_reserve(xyws_ctx* ctx, uint64_t max_batch_bytes, uint64_t max_frame
   if (!g.ok) return XYWS_ERR_HIP;
   if (max_batch_bytes > ctx->reserve_bytes) ctx->reserve_bytes = max_batch_bytes;
   if (max_frames > ctx->reserve_frames) ctx->reserve_frames = max_frames;
+  bool spare = true;  // the first unbound slot: the one the next new stream binds (acquire_slot)
   for (auto& sl : ctx->slot) {
     // the stream decoder's scratch (small: ~160 B per 128 KiB segment) in
-    // every slot; the per-frame tables only in slots bound to a stream now
-    // (the others get them when a stream binds them: acquire_slot)
+    // every slot; the per-frame tables in the slots bound to a stream now and
+    // in one spare, so that a stream first used inside graph capture finds
+    // them (the others get them when a stream binds them: acquire_slot)
     int rc = stream_scratch_reserve(&sl.ss, ctx->reserve_bytes);
     if (rc) return rc;
-    if (ctx->reserve_frames && sl.bound) {
+    const bool take = sl.bound || spare;
+    if (!sl.bound) spare = false;
+    if (ctx->reserve_frames && take) {
       if ((rc = ensure_table(&sl, ctx->reserve_frames, false))) return rc;
       if ((rc = stream_scratch_reserve_frames(&sl.ss, ctx->reserve_bytes, ctx->reserve_frames))) return rc;
     }
@@ -453,6 +457,17 @@ int xyws_unmask(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4], ui
   return hip_err(hipGetLastError());
 }
 
+int xyws_pointer_device(const void* p, int* device) {
+  if (!device) return XYWS_ERR_INVALID;
+  *device = -1;
+  if (!p) return XYWS_OK;
+  hipPointerAttribute_t attr;
+  const bool on_dev = hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeDevice;
+  (void)hipGetLastError();  // (an unregistered host pointer leaves an error behind)
+  if (on_dev) *device = attr.device;
+  return XYWS_OK;
+}
+
 // websocket_mask with the reference's contract (websocket_frame_mask.h:14,
 // called at example/include/common/websocket.h:131): host or device bytes,
 // done when it returns. Device bytes are unmasked in place; host bytes go
@@ -466,10 +481,10 @@ int xyws_mask_bytes(xyws_ctx* ctx, void* data, uint64_t len, const uint8_t key[4
   if (!g.ok) return XYWS_ERR_HIP;
   hipStream_t s = (hipStream_t)stream;
   if (capturing(s)) return XYWS_ERR_CAPACITY;  // (synchronous by contract)
-  hipPointerAttribute_t attr;
-  const bool on_dev = hipPointerGetAttributes(&attr, data) == hipSuccess && attr.type == hipMemoryTypeDevice;
-  (void)hipGetLastError();  // (an unregistered host pointer leaves an error behind)
-  if (on_dev) {
+  int pdev = -1;
+  if (const int rc = xyws_pointer_device(data, &pdev)) return rc;
+  if (pdev >= 0) {
+    if (pdev != ctx->device) return XYWS_ERR_INVALID;  // (another device's memory: its own context)
     if (const int rc = xyws_unmask(ctx, data, len, key, phase, nullptr, stream)) return rc;
     return hip_err(hipStreamSynchronize(s));
   }

@@ -55,6 +55,7 @@ struct arena_slot {
   uint8_t* host_meta;       // pinned: count (8 B) | carry (64 B)
   xyws_frame* dev_frames;
   uint64_t* dev_count;
+  hipEvent_t done;          // recorded after the submission's last copy: wait() syncs on it alone
 };
 
 struct arena_cb {
@@ -91,6 +92,7 @@ void arena_free(xyws_arena* a) {
     if (s.host_meta) (void)hipHostFree(s.host_meta);
     if (s.dev_frames) (void)hipFree(s.dev_frames);
     if (s.dev_count) (void)hipFree(s.dev_count);
+    if (s.done) (void)hipEventDestroy(s.done);
   }
   if (a->dev) (void)hipFree(a->dev);
   if (a->dev_carry) (void)hipFree(a->dev_carry);
@@ -190,6 +192,8 @@ int xyws_arena_create(xyws_ctx* ctx, void* host, uint64_t bytes, uint64_t max_fr
         hipMalloc(&s.dev_frames, a->max_frames * sizeof(xyws_frame)) != hipSuccess ||
         hipMalloc(&s.dev_count, 8) != hipSuccess)
       rc = XYWS_ERR_NOMEM;
+    else if (hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess)
+      rc = XYWS_ERR_HIP;
   }
   if (rc) {
     arena_free(a);
@@ -239,6 +243,7 @@ int xyws_arena_submit(xyws_arena* a, uint64_t offset, uint64_t len, uint32_t opt
   c.n = &a->note;
   c.seq = s_no;
   if (!rc && hipLaunchHostFunc(st, on_complete, &c) != hipSuccess) rc = XYWS_ERR_HIP;
+  if (!rc && hipEventRecord(s.done, st) != hipSuccess) rc = XYWS_ERR_HIP;
   if (rc) {
     a->failed = true;
     return rc;
@@ -265,7 +270,11 @@ int xyws_arena_poll(xyws_arena* a, uint64_t seq, xyws_arena_result* out) {
 int xyws_arena_wait(xyws_arena* a, uint64_t seq, xyws_arena_result* out) {
   if (!a || seq >= a->next_seq) return XYWS_ERR_INVALID;
   device_guard g(a->ctx->device);
-  if (hipStreamSynchronize(a->stream) != hipSuccess) return XYWS_ERR_HIP;
+  // the submission's own event, not the stream: arenas share the context's
+  // streams, and another connection's later work on this stream is not waited for
+  const arena_slot& s = a->slot[seq % XYWS_ARENA_SLOTS];
+  if (s.seq != seq) return XYWS_ERR_INVALID;
+  if (hipEventSynchronize(s.done) != hipSuccess) return XYWS_ERR_HIP;
   while (a->note.completed.load(std::memory_order_acquire) <= seq) usleep(10);  // (the callback runs after the sync)
   return xyws_arena_poll(a, seq, out);
 }

@@ -599,7 +599,8 @@ __global__ void __launch_bounds__(FT) k_classify(const uint8_t* src, uint64_t sr
   const bool proto = (f.status & (XYWS_ST_RSV | XYWS_ST_RESERVED_OPCODE | XYWS_ST_BAD_CONTROL)) != 0;
   uint16_t code = 0;
   if ((policy & XYWS_POL_STRICT) && proto) code = 1002;
-  else if (op == XYWS_FLAG_OP_CLOSE) code = 1000;  // (websocket.h:87-90, opcode compared exactly)
+  else if (op == XYWS_FLAG_OP_CLOSE || ((policy & XYWS_POL_REFERENCE) && (op & 8u)))
+    code = 1000;  // (websocket.h:87-90: the opcode compared exactly, or its bit 3 as the reference tests it)
   else if (!(f.flags & XYWS_FLAG_FIN) && !(policy & XYWS_POL_FRAGMENTS)) code = 1003;
   else if (!(f.flags & XYWS_FLAG_HAS_MASK) && !(policy & XYWS_POL_UNMASKED)) code = 1008;
   else if (f.payload_len > max_payload) code = 1009;
