@@ -237,9 +237,10 @@ void serve(int fd, uint64_t B, uint32_t opts, bool rfc, server_stats& st) {
   xyws_ctx_last_device_error(ctx, &derr);
   if (derr) die("device error word", (long)derr);
   ::shutdown(fd, SHUT_WR);
-  hipHostFree(hin); hipHostFree(hout); hipHostFree(hs); hipHostFree(hoffs);
-  hipFree(doffs); hipFree(din); hipFree(dout); hipFree(dframes); hipFree(dverd); hipFree(dcarry); hipFree(dsc);
-  hipStreamDestroy(s);
+  (void)hipHostFree(hin); (void)hipHostFree(hout); (void)hipHostFree(hs); (void)hipHostFree(hoffs);
+  (void)hipFree(doffs); (void)hipFree(din); (void)hipFree(dout); (void)hipFree(dframes); (void)hipFree(dverd);
+  (void)hipFree(dcarry); (void)hipFree(dsc);
+  (void)hipStreamDestroy(s);
   xyws_ctx_destroy(ctx);
 }
 

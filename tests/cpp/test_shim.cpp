@@ -10,7 +10,7 @@
 // tests/test_cpp_shim.py) so this program hard-codes no answers.
 //
 // usage: test_shim <vectors.txt>; prints one line per failure and "ok <n>".
-#include <hip/hip_runtime.h>
+#include <hip/hip_runtime_api.h>
 
 #include <cstdio>
 #include <cstring>

@@ -64,6 +64,7 @@ def test_unmask_captured_and_replayed(n, phase):
     orig = data.clone()
     mask = 0x1F2E3D4C
     view = data[5:]  # (misaligned start)
+    ws.context(0).reserve(n + 64)  # (the claim counter of a stream new to the context)
     s = torch.cuda.Stream()
     g = torch.cuda.CUDAGraph()
     torch.cuda.synchronize()

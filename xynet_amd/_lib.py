@@ -28,6 +28,8 @@ OPT_TEST_STEAL = 0x800000
 OPT_SWEEP = 0x1000000      # the sweep decoder (segment claiming) instead of the run decoder
 OPT_TEST_SPEC = 0x2000000  # sweep decoder tests: forced mis-speculation
 OPT_RUNS = 0x80000000      # the run decoder whatever the decoder choice would take
+OPT_LATTICE = 0x400        # the lattice decoder first (the run decoder after it takes what it leaves)
+OPT_NO_LATDEC = 0x800      # never the lattice decoder
 # debug stats indices (xyws_stream.hip)
 ST_RUNS, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRAMES = range(8)
 ST_GIVEUP, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS = 32, 33, 34, 35, 36

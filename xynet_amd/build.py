@@ -24,7 +24,7 @@ TARGETS = {
     "libxyws.so": ["xyws.hip", "xyws_stream.hip", "xyws_frames.hip", "xyws_arena.hip", "xyws_shard.hip"],
     "libxyws_tools.so": ["xyws_tools.hip"],
 }
-DEPS = ["xyws_device.h", "xyws_stream.h", "xyws_ctx.h"]
+DEPS = ["xyws_device.h", "xyws_stream.h", "xyws_ctx.h", "xyws_lattice.h"]
 
 
 def _stale(out, srcs):
@@ -56,7 +56,10 @@ def build(force=False, verbose=False, extra=None):
 
 # C++ callers of the header-only shim (include/xyws/websocket.hpp) and of the
 # C-ABI (the loopback echo harness), run by the GPU tests: linked against the in-tree libxyws.so (rpath), built here so the
-# binary travels to the GPU box with the tree.
+# binary travels to the GPU box with the tree. They are host code only (the
+# kernels are libxyws.so's), so g++ builds them, with the HIP runtime API
+# headers where they call it (hipcc's device pass crashed on the shim's
+# std::views::join overload: clang 22, ROCm 7.2).
 CPP_TESTS = {"tests/cpp/test_shim": "tests/cpp/test_shim.cpp", "tests/cpp/test_compat": "tests/cpp/test_compat.cpp",
              "examples/echo_loopback": "examples/echo_loopback.cpp"}
 
@@ -69,8 +72,10 @@ def build_cpp_tests(hipcc, force=False, verbose=False):
         if not force and os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
             continue
         rpath = os.path.relpath(PKG, os.path.dirname(out))
-        cmd = [hipcc, "-std=c++20", "-O2", "-Wall", "-I" + INC, src, "-o", out, "-L" + PKG, "-lxyws",
-               "-Wl,-rpath,$ORIGIN/" + rpath]
+        rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+        cmd = [os.environ.get("CXX", "g++"), "-std=c++20", "-O2", "-Wall", "-I" + INC, "-I" + rocm + "/include",
+               "-D__HIP_PLATFORM_AMD__", src, "-o", out, "-L" + PKG, "-lxyws", "-L" + rocm + "/lib", "-lamdhip64",
+               "-Wl,-rpath,$ORIGIN/" + rpath + ":" + rocm + "/lib"]
         if verbose:
             print(" ".join(cmd))
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -36,43 +36,100 @@
 #define UNMASK_LDS_FRAMES 512u
 
 // ---------------------------------------------------------------------------
-// k_unmask_range: dev[j] ^= K[(ph + j) % 4] over positions [lo, hi).
-// kw = aligned_key(K, lo, ph). Tiles of UNMASK_U x 256 chunks of 16 bytes per
-// workgroup (grid-stride): each lane issues its UNMASK_U nontemporal loads
-// before any XOR or store (memory-level parallelism: one load in flight per
-// lane left HBM half idle, 4.8 TB/s), then XORs and stores them; the two
-// edge chunks store only their in-range bytes.
+// k_unmask_range: dev[j] ^= K[(ph + j) % 4] over positions [lo, hi), the
+// device analogue of websocket_mask (websocket_frame_mask.h:14-24).
+// kw = aligned_key(K, lo, ph). Persistent workgroups (UNMASK_WPC per CU) claim
+// tiles of UNMASK_NT x UNMASK_U chunks of 16 bytes from one counter, one claim
+// ahead, and keep the next tile's nontemporal loads in flight while the
+// current tile is XORed and stored (a register double buffer): every CU
+// streams to the end of the range instead of a fixed share of it
+// (scripts/bw_probe7: the fixed 2048-block grid-stride form ran at 5.07 TB/s
+// R+W on the c3 batch). The two edge chunks store only their in-range bytes.
+// The last workgroup out resets the counter (graph replays start from zero).
+#define UNMASK_NT 256u
 #define UNMASK_U 8u
-__global__ void __launch_bounds__(256) k_unmask_range(uint8_t* __restrict__ base, uint64_t lo,
-                                                      uint64_t hi, uint32_t kw) {
-  const uint64_t c0 = lo >> 4, c1 = (hi + 15) >> 4;  // chunk range
-  const uint64_t tile = (uint64_t)UNMASK_U * 256u;
-  const uint64_t ntiles = (c1 - c0 + tile - 1) / tile;
-  u32x4* __restrict__ p = reinterpret_cast<u32x4*>(base);
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const uint64_t cb = c0 + t * tile + threadIdx.x;
-    u32x4 v[UNMASK_U];
-#pragma unroll
-    for (uint32_t u = 0; u < UNMASK_U; u++) {
-      const uint64_t c = cb + u * 256u;
-      const bool full = c < c1 && (c << 4) >= lo && (c << 4) + 16 <= hi;
-      v[u] = full ? __builtin_nontemporal_load(p + c) : u32x4{0u, 0u, 0u, 0u};
+#define UNMASK_WPC 4u
+__global__ void __launch_bounds__(UNMASK_NT) k_unmask_range(uint8_t* __restrict__ base, uint64_t lo, uint64_t hi,
+                                                            uint32_t kw, uint32_t* __restrict__ ctr) {
+  constexpr uint32_t TILE = UNMASK_NT * UNMASK_U;  // chunks per tile
+  const uint64_t c0 = lo >> 4, c1 = (hi + 15) >> 4;
+  const uint64_t ntiles = (c1 - c0 + TILE - 1) / TILE;
+  const uint32_t t = threadIdx.x;
+  __shared__ uint64_t s_tile;
+  uint64_t ahead = ~0ull;  // thread 0: the tile claimed one tile ahead
+  if (t == 0) {
+    const uint64_t a = atomicAdd(ctr, 1u);
+    s_tile = a < ntiles ? a : ~0ull;
+    if (a < ntiles) {
+      const uint64_t b = atomicAdd(ctr, 1u);
+      ahead = b < ntiles ? b : ~0ull;
     }
+  }
+  __syncthreads();
+  uint64_t cur = s_tile;
+  // chunk range [c0, c1) as buffer offsets from base + 16*c0; loads past it read
+  // zero, stores past it are dropped
+  const uint64_t nbytes = (c1 - c0) * 16;
+  auto rsrc = [&](uint64_t tile) {
+    const uint64_t off = tile * TILE * 16;
+    const uint64_t room = nbytes - off;
+    return __builtin_amdgcn_make_buffer_rsrc(base + c0 * 16 + off, 0,
+                                             room < TILE * 16 ? (uint32_t)room : TILE * 16, 0x00020000);
+  };
+  u32x4 e[UNMASK_U];
+  if (cur != ~0ull) {
+    const auto r = rsrc(cur);
+#pragma unroll
+    for (uint32_t u = 0; u < UNMASK_U; u++)
+      e[u] = __builtin_amdgcn_raw_buffer_load_b128(r, t * 16u, u * UNMASK_NT * 16u, 2);
+  }
+  while (cur != ~0ull) {
+    __syncthreads();  // (s_tile is rewritten below)
+    if (t == 0) {
+      s_tile = ahead;
+      if (ahead != ~0ull) {
+        const uint64_t b = atomicAdd(ctr, 1u);
+        ahead = b < ntiles ? b : ~0ull;
+      }
+    }
+    __syncthreads();
+    const uint64_t nx = s_tile;
+    u32x4 d[UNMASK_U];
+#pragma unroll
+    for (uint32_t u = 0; u < UNMASK_U; u++) d[u] = e[u] ^ kw;
+    if (nx != ~0ull) {
+      const auto r = rsrc(nx);
+#pragma unroll
+      for (uint32_t u = 0; u < UNMASK_U; u++)
+        e[u] = __builtin_amdgcn_raw_buffer_load_b128(r, t * 16u, u * UNMASK_NT * 16u, 2);
+    }
+    const auto w = rsrc(cur);
 #pragma unroll
     for (uint32_t u = 0; u < UNMASK_U; u++) {
-      const uint64_t c = cb + u * 256u;
-      if (c >= c1) continue;
+      const uint64_t c = c0 + cur * TILE + u * UNMASK_NT + t;  // absolute chunk
       const uint64_t a = c << 4;
-      if (a >= lo && a + 16 <= hi) {
-        u32x4 x = v[u];
-        x.x ^= kw; x.y ^= kw; x.z ^= kw; x.w ^= kw;
-        __builtin_nontemporal_store(x, p + c);
-      } else {
+      const bool whole = a >= lo && a + 16 <= hi;
+      __builtin_amdgcn_raw_buffer_store_b128(d[u], w, whole ? t * 16u : 0x80000000u, u * UNMASK_NT * 16u, 2);
+      // (the store's data registers stay live past the next store)
+      asm volatile("" ::"v"(d[u].x), "v"(d[u].y), "v"(d[u].z), "v"(d[u].w));
+      if (!whole && c < c1) {  // an edge chunk: its in-range bytes
         for (uint32_t b = 0; b < 16; b++) {
           const uint64_t q = a + b;
-          if (q >= lo && q < hi) base[q] ^= (uint8_t)(kw >> (8u * (b & 3u)));
+          const uint32_t wd = b < 4 ? d[u].x : b < 8 ? d[u].y : b < 12 ? d[u].z : d[u].w;
+          if (q >= lo && q < hi) base[q] = (uint8_t)(wd >> (8u * (b & 3u)));
         }
       }
+    }
+    asm volatile("s_nop 1" ::: "memory");
+    cur = nx;
+  }
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t n = atomicAdd(ctr + 1, 1u);
+    if (n + 1 == gridDim.x) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -436,13 +493,14 @@ int xyws_debug_policy(xyws_ctx* ctx, void* stream, uint64_t* out) {
   return XYWS_ERR_INVALID;
 }
 
-int xyws_unmask(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4], uint64_t phase,
-                uint64_t* phase_out, void* stream) {
-  if (!ctx || !key || (!dev && len)) return XYWS_ERR_INVALID;
-  if (phase_out) *phase_out = phase + len;
-  if (!len) return XYWS_OK;
-  device_guard g(ctx->device);
-  if (!g.ok) return XYWS_ERR_HIP;
+// xyws_unmask with ctx->mu held: the claim counter is the stream's scratch slot's.
+static int unmask_locked(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4], uint64_t phase,
+                         hipStream_t s) {
+  scratch_slot* sl = nullptr;
+  int rc = acquire_slot(ctx, s, capturing(s), &sl);
+  if (rc) return rc;
+  uint32_t* ctr = nullptr;
+  if ((rc = stream_scratch_unmask_counter(&sl->ss, capturing(s), &ctr))) return rc;
   const uintptr_t addr = reinterpret_cast<uintptr_t>(dev);
   uint8_t* base = reinterpret_cast<uint8_t*>(addr & ~(uintptr_t)15);
   const uint64_t lo = addr & 15, hi = lo + len;
@@ -452,9 +510,20 @@ int xyws_unmask(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4], ui
   const uint32_t c = (uint32_t)(phase - lo) & 3u;
   const uint32_t kw = c ? ((k >> (8u * c)) | (k << (32u - 8u * c))) : k;
   const uint64_t chunks = ((hi + 15) >> 4) - (lo >> 4);
-  hipLaunchKernelGGL(k_unmask_range, dim3(grid_for(chunks, 256 * UNMASK_U, 2048)), dim3(256), 0,
-                     (hipStream_t)stream, base, lo, hi, kw);
+  const uint32_t grid = grid_for(chunks, UNMASK_NT * UNMASK_U, (uint32_t)sl->ss.ncu * UNMASK_WPC);
+  hipLaunchKernelGGL(k_unmask_range, dim3(grid), dim3(UNMASK_NT), 0, s, base, lo, hi, kw, ctr);
   return hip_err(hipGetLastError());
+}
+
+int xyws_unmask(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4], uint64_t phase,
+                uint64_t* phase_out, void* stream) {
+  if (!ctx || !key || (!dev && len)) return XYWS_ERR_INVALID;
+  if (phase_out) *phase_out = phase + len;
+  if (!len) return XYWS_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  device_guard g(ctx->device);
+  if (!g.ok) return XYWS_ERR_HIP;
+  return unmask_locked(ctx, dev, len, key, phase, (hipStream_t)stream);
 }
 
 int xyws_pointer_device(const void* p, int* device) {
@@ -502,7 +571,7 @@ int xyws_mask_bytes(xyws_ctx* ctx, void* data, uint64_t len, const uint8_t key[4
   }
   // the stage keeps the bytes' 16-byte phase, so the kernel sees the same lanes
   if (hipMemcpyAsync(ctx->stage, data, len, hipMemcpyHostToDevice, s) != hipSuccess) return XYWS_ERR_HIP;
-  if (const int rc = xyws_unmask(ctx, ctx->stage, len, key, phase, nullptr, stream)) return rc;
+  if (const int rc = unmask_locked(ctx, ctx->stage, len, key, phase, s)) return rc;
   if (hipMemcpyAsync(data, ctx->stage, len, hipMemcpyDeviceToHost, s) != hipSuccess) return XYWS_ERR_HIP;
   return hip_err(hipStreamSynchronize(s));
 }

@@ -22,6 +22,8 @@ struct stream_scratch {
   // run decoder serves every call that does not ask for the sweep)
   volatile uint64_t* pol_h;
   uint64_t* pol_d;
+  void* lmem;           // lattice decoder: scratch words + one result word per segment
+  uint64_t lmax_segs;
 };
 
 void stream_scratch_init(stream_scratch* s, int device);
@@ -35,6 +37,9 @@ uint32_t stream_scratch_error(stream_scratch* s, bool clear);
 #define XYWS_NSTATS 48
 int stream_scratch_stats(stream_scratch* s, uint64_t out[XYWS_NSTATS]);
 int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_runs);
+// xyws_unmask's claim counter pair (u32 claims, u32 workgroups done; zeroed at
+// allocation, reset by the kernel's last workgroup) in this scratch
+int stream_scratch_unmask_counter(stream_scratch* s, bool capturing, uint32_t** out);
 
 // Internal decode options (not part of include/xyws.h):
 #define XYWS_OPT_STATS 0x100u      // count speculation/repair events (xyws_debug_stats)
@@ -63,6 +68,10 @@ int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_ru
 #define XYWS_OPT_SWX_NOREC 0x20000000u  // timing experiments only: no segment records
 #define XYWS_OPT_SW_LOADWAIT 0x40000000u  // experiment (sweep): the next segment's loads land before the stores issue
 #define XYWS_OPT_RUNS 0x80000000u     // the run decoder, whatever the decoder choice would take
+#define XYWS_OPT_LATTICE 0x400u      // the lattice decoder first, whatever the decoder choice would take
+#define XYWS_OPT_NO_LATDEC 0x800u    // never the lattice decoder
+#define XYWS_OPT_REDIRECT 0x2000u    // (set by stream_decode_fused only) the run decoder after the lattice decoder:
+                                     // it reads the lattice's redirect record first
 #define XYWS_OPT_TEST_SPEC 0x2000000u  // tests (sweep decoder): segments 1, 4, 7, ... report no entry, segments
                                        // 2, 5, 8, ... speculate one byte late (look-back fix-ups, repair walk)
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
