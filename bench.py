@@ -358,7 +358,7 @@ def source_hash():
     so that a traffic figure is only reported for the kernel it was measured on."""
     import hashlib
     h = hashlib.sha256()
-    for f in ("xyws_stream.hip", "xyws_device.h", "xyws_stream.h", "xyws.hip"):
+    for f in ("xyws_stream.hip", "xyws_device.h", "xyws_stream.h", "xyws.hip", "xyws_lattice.h"):
         with open(os.path.join(ROOT, "xynet_amd", "csrc", f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
@@ -672,7 +672,7 @@ def main():
     # steps see the device's steady state. A burst of 2 GiB decodes runs
     # through a power/clock transient: the sweep decoder's kernel time rises
     # from ~710 to ~850 us over its first few calls and settles at ~695 us
-    # after ~18 (profiles/r03j_c3_dispatch_sequence.json, r03k); the timed
+    # after ~18 (profiles/archive/r03j_c3_dispatch_sequence.json, r03k); the timed
     # region is unchanged (exactly K steps), the count is in the JSON line.
     settle = max(0, args.settle - args.warmup)
     for i in range(settle + args.warmup):
@@ -704,7 +704,8 @@ def main():
         pol = (C.c_uint64 * 5)()
         if dec.ctx.L.xyws_debug_policy(dec.ctx.h, C.c_void_p(stream.cuda_stream), pol) == 0:
             decoder = {0: "runs (k_stream_runs)", 1: "sweep (k_stream_sweep)",
-                       2: "runs (k_stream_runs, 512-thread workgroups, 64 KiB segments)"}.get(int(pol[4]) & 3)
+                       2: "runs (k_stream_runs, 512-thread workgroups, 64 KiB segments)",
+                       3: "lattice (k_stream_lattice)"}.get(int(pol[4]) & 3)
 
     if args.stats and rank == 0:  # two extra decodes of copy 0 (keeps its parity)
         names = ["runs", "runs_without_entry", "bad_boundaries", "repairs", "cuts", "spins", "dense_passes",
