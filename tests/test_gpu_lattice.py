@@ -29,7 +29,10 @@ pytestmark = pytest.mark.gpu
 
 OPT_LATTICE = 0x400
 OPT_SMALL = 0x200
-MODES = {"lat": {"opts": OPT_LATTICE}, "lat1k": {"opts": OPT_LATTICE | OPT_SMALL}}
+OPT_TEST_LATSPEC = 0x10  # every store speculative: a broken lattice is undone by the end-of-work check
+MODES = {"lat": {"opts": OPT_LATTICE}, "lat1k": {"opts": OPT_LATTICE | OPT_SMALL},
+         "lat_blind": {"opts": OPT_LATTICE | OPT_TEST_LATSPEC},
+         "lat1k_blind": {"opts": OPT_LATTICE | OPT_SMALL | OPT_TEST_LATSPEC}}
 
 
 @pytest.fixture(scope="module")
@@ -160,12 +163,14 @@ def test_irregular_streams(ws, oracle, mode):
 def test_lattice_then_irregular_then_lattice(ws, oracle):
     """The decoder choice without forcing: regular batches take the lattice,
     an irregular one after them is redirected at its first size change, the
-    next regular one takes the lattice again (policy word 4: 3 = lattice)."""
+    next irregular one takes the run decoder, and a regular one after that
+    the run decoder once more (the choice follows the previous call), then the
+    lattice again (policy word 4: 3 = lattice)."""
     dec = ws.frame_decoder()
-    reg = regular(1, 4096, 500)
+    reg = regular(1, 256, 8000)  # (equal frames of up to LAT_FAUTO bytes)
     irr = streams.case_bytes("random_frames_300")
     used = []
-    for src in (reg, reg, irr, irr, reg):
+    for src in (reg, reg, irr, irr, reg, reg):
         view, _ = dev_bytes(src)
         ob = np.frombuffer(src, np.uint8).copy()
         ofr, _, on = oracle.decode_stream(ob)
@@ -174,4 +179,4 @@ def test_lattice_then_irregular_then_lattice(ws, oracle):
         assert host(view) == ob.tobytes()
         assert frames_list(r.frames(), True) == frames_list(ofr, True)
         used.append(_policy(dec)[4])
-    assert used[1] == 3 and used[4] == 3 and used[3] != 3  # (call 0 follows whatever ran before on the stream)
+    assert used[1] == 3 and used[3] != 3 and used[4] != 3 and used[5] == 3  # (call 0 follows the stream's past)

@@ -43,12 +43,15 @@
 // ahead, and keep the next tile's nontemporal loads in flight while the
 // current tile is XORed and stored (a register double buffer): every CU
 // streams to the end of the range instead of a fixed share of it
-// (scripts/bw_probe7: the fixed 2048-block grid-stride form ran at 5.07 TB/s
-// R+W on the c3 batch). The two edge chunks store only their in-range bytes.
-// The last workgroup out resets the counter (graph replays start from zero).
-#define UNMASK_NT 256u
-#define UNMASK_U 8u
-#define UNMASK_WPC 4u
+// (scripts/bw_probe7 on the c3 batch, R+W: the fixed 2048-block grid-stride
+// form 5.34 TB/s; claimed 64 KiB tiles of 1024 threads x 4 chunks, two
+// workgroups per CU, 6.42 TB/s — the probe's best, with 1024 x 8 x 1 at 6.40;
+// 256-thread tiles 5.0-5.7). The two edge chunks store only their in-range
+// bytes. The last workgroup out resets the counter (graph replays start from
+// zero).
+#define UNMASK_NT 1024u
+#define UNMASK_U 4u
+#define UNMASK_WPC 2u
 __global__ void __launch_bounds__(UNMASK_NT) k_unmask_range(uint8_t* __restrict__ base, uint64_t lo, uint64_t hi,
                                                             uint32_t kw, uint32_t* __restrict__ ctr) {
   constexpr uint32_t TILE = UNMASK_NT * UNMASK_U;  // chunks per tile

@@ -47,35 +47,49 @@
 
 constexpr uint64_t LAT_FMIN = 128;          // smaller frames: the run decoder (its dense pass)
 constexpr uint64_t LAT_FMAX = 1ull << 40;   // (lattice arithmetic stays well inside 64 bits)
+constexpr uint64_t LAT_FAUTO = 1024;        // the decoder choice takes the lattice for equal frames up to this size
 // lattice scratch (u64 words, zeroed at allocation)
 enum {
   LW_CNT = 0,      // u32 [0] claim counter, u32 [1] done count (reset by the finisher)
   LW_EPOCH = 1,    // completed calls (a call runs with E = this + 1)
   LW_BRK = 2,      // ~(earliest failing lattice index) of this call, 0 = none (reset by the finisher)
   LW_UNMASK = 3,   // xyws_unmask's claim counter pair (u32 claims, u32 done; reset by its last workgroup)
+  LW_W = 4,        // the decided prefix: every segment below it has published its result (reset by the finisher)
   LW_REDIR = 8,    // redirect record for the run decoder: [0] state, [1] p, [2] frames before p
   LW_RCARRY = 16,  // the carry the run decoder starts from at p (8 words)
   LW_STAT = 32     // per segment: (E << 2) | LS_*
 };
-enum { LS_AGG = 1, LS_INCL = 2, LS_BRK = 3 };
+enum { LS_AGG = 1, LS_BRK = 3 };
+constexpr uint32_t LAT_SLIST = 512;  // speculative stores a workgroup records for its end-of-work check
 enum : uint64_t { RD_DONE = 0, RD_FULL = 1, RD_FROM = 2 };
 
-template <uint32_t NT_, uint32_t SEG_>
+template <uint32_t NT_, uint32_t SEG_, uint32_t WPC_ = 1>
 struct lgeom {
-  static constexpr uint32_t NT = NT_, SEG = SEG_, CH = SEG_ / 16 / NT_;
+  static constexpr uint32_t NT = NT_, SEG = SEG_, WPC = WPC_;  // WPC: workgroups per CU
   static constexpr uint32_t TMAX = SEG_ / LAT_FMIN + 3;  // covering frame + lattice points
-  static_assert(CH * 16 * NT == SEG, "whole chunks per lane");
 };
-using G_LAT = lgeom<1024, 131072>;
+// 56 KiB segments: 8 rows of 1 KiB for each of the 7 data waves (no partial
+// last round: every wave's loads and stores are unconditional), two
+// workgroups per CU (one streams while the other checks, XORs and decides)
+using G_LAT = lgeom<1024, 15 * 8 * 1024, 1>;
+// (experiment, XYWS_OPT_LATX_2WG: 56 KiB segments for 7 data waves, two
+// 512-thread workgroups per CU)
+using G_LAT2 = lgeom<512, 7 * 8 * 1024, 2>;
 using G_LAT_SMALL = lgeom<64, 1024>;  // tests: 1 KiB segments, many segment boundaries
 
 template <class G>
 struct __attribute__((aligned(16))) lat_lds {
-  uint8_t seg[G::SEG + 32];  // the segment and the 16 bytes after it
+  // the segment, the 16 bytes after it, and the 20 bytes at the dword at or
+  // below the header of the frame covering its first bytes
+  uint8_t seg[G::SEG + 48];
   uint4 tab[G::TMAX];        // frames overlapping the segment: {ps, end, kw, 0} segment-relative
   cstate S0;                 // the state at the batch start (carry)
-  uint64_t E, X0, F, kmax, c0, brk_g;
-  uint32_t na, cur, nxt, brk, go, quit, done_last;
+  uint64_t E, X0, F, kmax, c0, kbf;
+  uint64_t gk;  // ~(the failing lattice index known to the control wave), 0 = none
+  uint32_t na, cur, nxt, brk, quit, done_last, nsl;
+  // speculatively stored segments of this workgroup and the lattice index
+  // their stores stop at (checked once every earlier segment has decided)
+  uint64_t sl_seg[LAT_SLIST], sl_k[LAT_SLIST];
 };
 
 // Segment-relative clamp of an absolute position to [0, 2^32).
@@ -85,39 +99,70 @@ XYWS_DEV uint32_t lat_rel(uint64_t x, uint64_t ss) {
   return d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
 }
 
-// The decoupled look-back of segment s (wave 0, every lane; the result in
-// every lane): 1 when every lattice point before segment s held (an INCL
-// among the predecessors with only AGG between), 0 when one failed (a BRK, or
-// a failing index before the segment in LW_BRK). Segments are claimed only by
-// running workgroups and a segment's result depends on nothing but its own
-// bytes, so every wait ends; the bound reports a bug (device error bit 2).
-XYWS_DEV int lat_lookback(const run_params& P, uint64_t s, uint64_t E, uint64_t k_first, uint32_t lane) {
-  if (s == 0) return 1;
-  const uint64_t* stat = P.lat + LW_STAT;
-  uint64_t j = s;
-  for (uint32_t it = 0; it < (1u << 22); it++) {
-    const uint64_t b = st_load(P.lat + LW_BRK);
-    if (b && ~b < k_first) return 0;  // a point before this segment failed
-    const bool valid = j >= 1 + (uint64_t)lane;
-    const uint64_t v = valid ? st_load(stat + (j - 1 - lane)) : ((E << 2) | LS_INCL);
-    const bool pub = (v >> 2) == E;
-    const uint32_t st = (uint32_t)v & 3u;
-    const uint64_t stop = __ballot(!pub || st >= LS_INCL);
-    if (!stop) {
-      j -= 64;  // 64 predecessors whose own points held: further back
-      continue;
-    }
-    const uint32_t f = (uint32_t)__builtin_ctzll(stop);
-    const uint64_t vf = shfl64(v, f);
-    if ((vf >> 2) != E) {  // the nearest undecided predecessor: wait for it
-      __builtin_amdgcn_s_sleep(1);
-      j = s;
-      continue;
-    }
-    return ((uint32_t)vf & 3u) == LS_INCL ? 1 : 0;
+// Segments per decided-prefix group: a segment adds one to its group's
+// counter (P.lgrp, reset by the finisher) after publishing its result, so a
+// full counter says 64 segments decided in one load.
+constexpr uint32_t LAT_GRP = 64;
+XYWS_DEV uint64_t lat_grp_size(const run_params& P, uint64_t g) {
+  const uint64_t a = g * LAT_GRP;
+  return a >= P.nseg ? 0 : (P.nseg - a < LAT_GRP ? P.nseg - a : LAT_GRP);
+}
+
+// The decided prefix (wave 0, every lane; the result in every lane): from
+// LW_W on, the full groups (64 counters at once: 4096 segments), then the
+// segments of the next group (4 statuses per lane: 256), raising LW_W past
+// what is decided. Ordering without fences (an agent-scope release fence is
+// a write-back of the XCD's whole L2 on gfx950, buffer_wbl2 sc1): every word
+// here is read and written at the coherence point (agent-scope atomics, sc1),
+// and each operation is issued after the one it depends on has completed — a
+// segment raises LW_BRK with a returning atomic before it publishes its
+// result and counts in its group, the raise of LW_W follows the loads of the
+// results it covers, and a reader of LW_W loads LW_BRK after it — so a
+// workgroup that sees LW_W > s reads in LW_BRK every failing point of
+// segments <= s.
+XYWS_DEV uint64_t lat_advance(const run_params& P, uint64_t E, uint32_t lane) {
+  const uint64_t w = uniform64(st_load(P.lat + LW_W));
+  if (w >= P.nseg) return w;
+  uint64_t w1 = w;
+  {
+    const uint64_t g0 = w / LAT_GRP, g = g0 + lane, gs = lat_grp_size(P, g);
+    const bool full = !gs || st_load(P.lgrp + g) == gs;
+    const uint64_t nf = __ballot(!full);
+    const uint32_t c = nf ? (uint32_t)__builtin_ctzll(nf) : 64u;
+    const uint64_t wg = (g0 + c) * LAT_GRP;
+    if (wg > w1) w1 = wg < P.nseg ? wg : P.nseg;
   }
-  if (lane == 0) atomicOr(P.head + 1, 2u);
-  return 0;
+  if (w1 < P.nseg) {
+    bool dec[4];
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) {
+      const uint64_t j = w1 + 4 * lane + r;
+      dec[r] = j >= P.nseg || (st_load(P.lat + LW_STAT + j) >> 2) == E;
+    }
+    // the lane's first undecided status, then the first lane with one
+    const uint32_t lc = !dec[0] ? 0u : !dec[1] ? 1u : !dec[2] ? 2u : !dec[3] ? 3u : 4u;
+    const uint64_t nd = __ballot(lc < 4);
+    uint64_t w2 = w1 + 256;
+    if (nd) {
+      const uint32_t f = (uint32_t)__builtin_ctzll(nd);
+      w2 = w1 + 4 * f + (uint32_t)__shfl((int)lc, (int)f, 64);
+    }
+    w1 = w2 < P.nseg ? w2 : P.nseg;
+  }
+  if (w1 > w && lane == 0) __hip_atomic_fetch_max(P.lat + LW_W, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return w1;
+}
+// Wait (wave 0) until every segment up to s has decided; bounded (device
+// error bit 2). Every segment at or below s was claimed by a running
+// workgroup and decides on its own bytes, so the wait ends.
+XYWS_DEV void lat_wait_decided(const run_params& P, uint64_t E, uint64_t s, uint32_t lane) {
+  for (uint32_t it = 0; lat_advance(P, E, lane) <= s; it++) {
+    if (it >= (1u << 20)) {
+      if (lane == 0) atomicOr(P.head + 1, 2u);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(8);  // (polls at the coherence point: spaced)
+  }
 }
 
 // XOR mask of the 16-byte chunk at segment offset a from the table: entry
@@ -229,6 +274,7 @@ XYWS_DEV void lat_finish(const run_params& P, lat_lds<G>& L) {
   }
   uint32_t* cnt = reinterpret_cast<uint32_t*>(P.lat + LW_CNT);
   st_store(P.lat + LW_BRK, 0);
+  st_store(P.lat + LW_W, 0);
   __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   st_store(P.lat + LW_EPOCH, L.E);
@@ -267,14 +313,455 @@ XYWS_DEV bool lat_redirect(run_params& P) {
   return true;
 }
 
+// Roles (as in the sweep decoder, sweep_io): in the production geometry wave
+// 0 is the CONTROL wave — claims, the covering frame's header and the 16 bytes
+// after the segment (loaded one segment ahead), the published results and the
+// look-back — and never loads or stores segment bytes, so its memory
+// operations never wait behind a segment's loads (vmcnt counts a wave's
+// operations in issue order); waves 1..15 move the data, one 1 KiB row per
+// wave instruction. In the one-wave test geometry wave 0 does both.
 template <class G>
-__global__ void __launch_bounds__(G::NT, 1) k_stream_lattice(run_params P) {
+struct lat_io {
+  static constexpr bool CTRL = G::NT >= 256;
+  static constexpr uint32_t NW = G::NT / 64, NDW = CTRL ? NW - 1 : NW;
+  static constexpr uint32_t NROW = G::SEG / 1024, K = (NROW + NDW - 1) / NDW;
+  static constexpr uint32_t CLAIM = CTRL ? 64u : 0u;  // the claim lane: lane 0 of the first data wave
+  static_assert(G::SEG % 1024 == 0, "segments are whole 1 KiB rows");
+  XYWS_DEV static bool data_wave(uint32_t wave) { return !CTRL || wave != 0; }
+  XYWS_DEV static uint32_t row(uint32_t wave, uint32_t k) { return (CTRL ? wave - 1 : wave) + NDW * k; }
+  XYWS_DEV static bool valid(uint32_t wave, uint32_t k) { return K * NDW == NROW || row(wave, k) < NROW; }
+};
+
+// An agent-coherent load whose value is used a segment later: inline asm, so
+// that the compiler neither waits for it nor counts it (the control wave waits
+// for all of its operations at once, a segment later: lat_loop).
+XYWS_DEV uint64_t lat_load_late(const uint64_t* p) {
+  uint64_t v;
+  asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+// The claim wave's extra loads for segment s, one dword per lane, issued with
+// its rows: lanes 0..3 the 16 bytes after the segment, lanes 4..8 the 20
+// bytes at the dword at or below the header of the frame covering the
+// segment's first bytes (lattice point ka-1) — lane i's dword goes to
+// L.seg[SEG + 4i]. One register (a load into registers
+// the compiler also pairs with others made it wait for every load in flight).
+// Dwords at or past the batch's last one read that one instead (each address
+// stays on the batch's pages; the readers cut at hi).
+XYWS_DEV uint32_t lat_ctrl_load(const run_params& P, uint64_t s, uint64_t SEGB, uint64_t X0, uint64_t F, uint64_t kmax,
+                                uint32_t tid) {
+  const uint64_t ss = s * SEGB;
+  const uint64_t ka = ss <= X0 ? 0 : (ss - X0 + F - 1) / F;
+  const uint64_t xc = ka && ka <= kmax ? X0 + (ka - 1) * F : ss;
+  const uint64_t top = (P.hi + 3) & ~3ull;
+  // (lane offsets from the per-segment opaque tid: 32-bit, not hoisted)
+  const uint32_t lane = tid & 63u;
+  const bool pd = lane < 4;
+  uint64_t q = (pd ? ss + SEGB : xc & ~3ull) + (uint32_t)(pd ? 4u * lane : 4u * (lane - 4u));
+  if (q + 4 > top) q = top - 4;
+  return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(P.base + q));
+}
+
+// The segment loop of one role (lat_io): the control lane's claims, loads,
+// results and look-back (ROLE CTRL), the data waves' loads, checks, XOR and
+// stores (DATA), or both (ALL: the one-wave geometry). Both loops meet the
+// same four barriers per segment (A: LDS free, B: segment in LDS, C: table
+// and checks done, D: the look-back's answer), so the control wave's state
+// and the data waves' prefetch registers never share a register allocation
+// region (one loop holding both spilled the prefetch, as in sweep_loop).
+enum { LR_ALL = 0, LR_CTRL = 1, LR_DATA = 2 };
+// stats mode (XYWS_OPT_STATS): shader clocks summed over workgroups, per phase,
+// for the control lane (tid 0) and one data lane (tid 64) — the debug stats
+// words from 16 on (the run decoder's timing slots; it does not run in a call
+// the lattice finished)
+enum { LT_C_A = 16, LT_C_C, LT_C_ADV, LT_D_FILL, LT_D_WB, LT_D_TAB, LT_D_WC, LT_D_MASK, LT_D_WD, LT_D_ST, LT_D_WA,
+       LT_SEGS, LT_GATE, LT_END };
+struct lat_clock {
+  bool on;
+  uint64_t t, acc[16];
+  XYWS_DEV void start(bool o) {
+    on = o;
+    for (int i = 0; i < 16; i++) acc[i] = 0;
+    t = on ? __builtin_amdgcn_s_memtime() : 0;
+  }
+  XYWS_DEV void mark(int slot) {
+    if (!on) return;
+    const uint64_t n = __builtin_amdgcn_s_memtime();
+    acc[slot - 16] += n - t;
+    t = n;
+  }
+  XYWS_DEV void flush(const run_params& P) {
+    if (!on) return;
+    for (int i = 0; i < 16; i++)
+      if (acc[i]) stat_add(P, 16 + i, acc[i]);
+  }
+};
+template <class G, int ROLE>
+XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32_t ahead) {
+  using IO = lat_io<G>;
+  constexpr bool CT = ROLE != LR_DATA, DT = ROLE != LR_CTRL;
+  uint32_t tid = tid0;
+  asm volatile("" : "+v"(tid));  // (lane address math per segment: see sweep_loop)
+  const uint32_t lane = tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(P.lat + LW_CNT);
+  const uint64_t E = uniform64(L.E);
+  const uint64_t X0 = uniform64(L.X0), F = uniform64(L.F), kmax = uniform64(L.kmax);
+  const float rF = 1.0f / (float)(F < (1ull << 24) ? F : (1ull << 24));
+  const uint32_t F32 = F < 0x80000000ull ? (uint32_t)F : 0x80000000u;
+  uint32_t cur = uniform32(L.cur);
+  uint32_t it = 0, nsl = 0;  // segments done; speculative stores recorded (every thread)
+  lat_clock clk;
+  clk.start(stats_on(P) && (tid == 0 || (tid == 64 && DT)));
+  uint64_t brk_seen = 0;                        // control lane: LW_BRK as loaded one segment ago
+  const bool cl = tid == 0 && CT;  // (which lane's clock this is: control or data)
+  u32x4 e[DT ? IO::K : 1];
+  uint32_t cx = 0;  // claim wave: lat_ctrl_load's dword
+  constexpr uint32_t CW = IO::CLAIM / 64u;
+  // a segment's loads: the claim wave first claims the segment after it (the
+  // atomic's value is read a segment later, inline asm: the compiler would
+  // wait for it at once) and loads the covering header and the bytes after
+  // it; then every data wave its rows, the youngest loads (the fill waits for
+  // them, and so for everything before them)
+  auto issue = [&](uint32_t s, bool claim) {
+    if constexpr (DT) {
+      if (wave == CW) {
+        if (lane == 0) {
+          if (claim)
+            asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(ahead) : "v"(cnt), "v"(1u) : "memory");
+          else
+            ahead = NONE32;
+        }
+        cx = lat_ctrl_load(P, s, G::SEG, X0, F, kmax, tid);
+      }
+      const __amdgpu_buffer_rsrc_t rs = lat_rsrc(P, (uint64_t)s * G::SEG, G::SEG);
+#pragma unroll
+      for (uint32_t k = 0; k < IO::K; k++)
+        e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, IO::valid(wave, k) ? lane * 16u : OOB,
+                                                     IO::row(wave, k) * 1024u, AUX_NT);
+    }
+  };
+  if (DT && cur != NONE32) {
+    const uint32_t a0 = ahead;
+    issue(cur, false);
+    ahead = a0;  // (claimed at the start)
+    // K dropped stores (out-of-range offset, no traffic) after the first
+    // loads, as after every later segment's: the fill's waits then count the
+    // stores younger than the loads on every path into the loop (sweep_loop)
+    const __amdgpu_buffer_rsrc_t rs = lat_rsrc(P, (uint64_t)cur * G::SEG, G::SEG);
+#pragma unroll
+    for (uint32_t k = 0; k < IO::K; k++)
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rs, OOB, k * 1024u, AUX_ST);
+  }
+  // the data lanes number the lattice points of a segment among themselves
+  const uint32_t dl = IO::CTRL ? tid - 64u : tid, NDL = IO::NDW * 64u;
+  while (cur != NONE32) {
+    asm volatile("" : "+v"(tid));
+    const uint64_t ss = (uint64_t)cur * G::SEG;
+    const uint64_t se = ss + G::SEG;
+    const uint64_t ka = ss <= X0 ? 0 : (ss - X0 + F - 1) / F;
+    clk.mark(cl ? LT_C_ADV : LT_D_ST);
+    __syncthreads();  // (A) the previous segment's LDS reads are done
+    clk.mark(cl ? LT_C_ADV : LT_D_WA);
+    if constexpr (DT) {
+#pragma unroll
+      for (uint32_t k = 0; k < IO::K; k++)
+        if (IO::valid(wave, k)) *reinterpret_cast<u32x4*>(&L.seg[IO::row(wave, k) * 1024u + lane * 16u]) = e[k];
+      if (clk.on) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (DT && wave == CW) {
+      // the claim and the control loads were issued just before this
+      // segment's rows: landed with them (a use of the last row's register
+      // orders the claim's inline-asm value after that wait)
+      asm volatile("" : "+v"(ahead), "+v"(cx) : "v"(e[IO::K - 1].x));
+      const uint32_t ln = tid & 63u;  // (from the per-segment opaque tid: not hoisted)
+      if (ln < 9) *reinterpret_cast<uint32_t*>(&L.seg[G::SEG + 4u * ln]) = cx;
+      if (lane == 0) {
+        L.nxt = ahead < P.nseg ? ahead : NONE32;  // (claimed a segment ago)
+        L.brk = NONE32;
+      }
+    }
+    clk.mark(cl ? LT_C_A : LT_D_FILL);
+    __syncthreads();  // (B)
+    clk.mark(cl ? LT_C_A : LT_D_WB);
+    const uint32_t nxt = uniform32(L.nxt);
+    uint64_t kz = se <= X0 ? 0 : (se - X0 + F - 1) / F;
+    if (kz > kmax) kz = kmax;
+    const uint32_t nl = kz > ka ? (uint32_t)(kz - ka) : 0u;
+    if constexpr (DT) {
+      if (tid == IO::CLAIM) {
+        // the frame covering the segment's first bytes (entry 0)
+        uint4 c = {0u, 0u, 0u, 0u};
+        if (ka == 0) {
+          const cstate S0 = L.S0;
+          if (!(S0.st & S_NOCOV)) c = uint4{lat_rel(S0.cov_ps, ss), lat_rel(X0, ss), S0.cov_kw, 0u};
+        } else if (ka <= kmax) {
+          const uint64_t xc = X0 + (ka - 1) * F;
+          const uint32_t sh = (uint32_t)(xc & 3);
+          uint32_t w[4];
+          const uint32_t* cw = reinterpret_cast<const uint32_t*>(&L.seg[G::SEG + 16]);
+#pragma unroll
+          for (int i = 0; i < 4; i++) w[i] = __builtin_amdgcn_alignbyte(cw[i + 1], cw[i], sh);
+          const uint64_t room = P.hi - xc;
+          const hdr_info h = parse_header_words(w, room < 16 ? (uint32_t)room : 16u);
+          if (h.hlen) {
+            const uint64_t ps = xc + h.hlen;
+            const uint64_t end = ka == kmax ? sat_add(ps, h.plen) : xc + F;
+            c = uint4{lat_rel(ps, ss), lat_rel(end < P.hi ? end : P.hi, ss), aligned_key(h.key, ps, 0), 0u};
+          }
+        }
+        L.tab[0] = c;
+      }
+      if (nxt != NONE32) issue(nxt, !L.quit);  // (in flight through the checks, the look-back and the stores)
+      // lattice points in the segment: k in [ka, kz), each checked by one data lane
+      const uint32_t nlw = (P.opts & XYWS_OPT_LATX_NOWORK) ? 0u : nl;  // (timing experiment)
+      for (uint32_t i = dl; i < nlw; i += NDL) {
+        const uint64_t k = ka + i;
+        const uint64_t x = X0 + k * F;
+        const uint32_t xr = (uint32_t)(x - ss);
+        const hdr_info h = lat_hdr(P, L.seg, xr, x);
+        const bool last = k + 1 == kmax;
+        const uint64_t fend = h.hlen ? sat_add(x + h.hlen, h.plen) : x;
+        // the point holds: a frame of exactly F bytes, or the batch's last
+        // frame (cut by the batch end, or a header the end cuts)
+        const bool ok = h.hlen ? ((uint64_t)h.hlen + h.plen == F && h.plen < F) || (last && fend >= P.hi) : last;
+        if (!ok) atomicMin(&L.brk, i);
+        uint4 en = {xr, xr, 0u, 0u};
+        if (h.hlen) {
+          const uint64_t ps = x + h.hlen;
+          en = uint4{lat_rel(ps, ss), lat_rel(fend < P.hi ? fend : P.hi, ss), aligned_key(h.key, ps, 0), 0u};
+        }
+        L.tab[1 + i] = en;
+      }
+    }
+    // (B..C) the control lane: every operation it issued a segment ago (its
+    // load of LW_BRK, the status store, the group count) has completed: one
+    // wait, then the failing point known from LW_BRK as loaded then (stale by
+    // a segment: speculation, checked at the end of the work) for this
+    // segment's stores
+    if (CT && tid == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(brk_seen)::"memory");
+      if (cl) clk.mark(LT_GATE);  // (stats: the control wave's wait for its operations of a segment ago)
+      L.gk = brk_seen;
+    }
+    clk.mark(cl ? LT_C_A : LT_D_TAB);
+    __syncthreads();  // (C) the table and the segment's own checks are complete
+    clk.mark(cl ? LT_C_C : LT_D_WC);
+    const uint32_t brk = uniform32(L.brk);
+    // the workgroup's first segment waits for every earlier one to decide
+    // (they are all in their first segment too: a failing point near the
+    // batch start is seen before any store, so a miss stores nothing)
+    // (XYWS_OPT_TEST_LATSPEC: no gate and no LW_BRK filter, so that a broken
+    // lattice stores past its failing point and the end-of-work check undoes
+    // it)
+    const bool blind = (P.opts & XYWS_OPT_TEST_LATSPEC) != 0;
+    const bool gate = it == 0 && !blind;
+    if (CT && tid < 64) {
+      // the segment's own result, published while the data waves store
+      if (tid == 0) {
+        // (a returning atomic, its value used: performed before the result is published)
+        if (brk != NONE32) {
+          uint64_t o = __hip_atomic_fetch_max(P.lat + LW_BRK, ~(ka + brk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" : "+v"(o)::"memory");
+        }
+        st_store(P.lat + LW_STAT + cur, (E << 2) | (brk != NONE32 ? LS_BRK : LS_AGG));
+        __hip_atomic_fetch_add(P.lgrp + cur / LAT_GRP, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (gate) {
+        lat_wait_decided(P, E, cur, lane);
+        if (tid == 0) L.gk = st_load(P.lat + LW_BRK);
+      }
+      // the load for the next segment's decision (the last operation of the
+      // phase: used a segment later)
+      if (tid == 0) brk_seen = lat_load_late(P.lat + LW_BRK);
+    }
+    if (gate) __syncthreads();  // (D, the first segment only) the fresh failing point
+    clk.mark(cl ? LT_C_C : LT_D_WD);
+    // where the segment's stores stop: its own failing point or an earlier
+    // one known (every thread: the same uniform arithmetic)
+    const uint64_t b = blind ? 0 : uniform64(L.gk);
+    uint64_t kst = brk != NONE32 ? ka + brk : kz;
+    if (b && ~b < kst) kst = ~b;
+    uint32_t stop = kst >= kz ? G::SEG : lat_rel(X0 + kst * F, ss);  // (kst <= kmax: inside the lattice's span)
+    if (stop > G::SEG) stop = G::SEG;
+    bool quit = b || brk != NONE32;  // the rest of the batch is the run decoder's
+    // a store not known valid now is checked at the end (gate: known)
+    if (stop && !gate) {
+      if (nsl < LAT_SLIST) {
+        if (tid == IO::CLAIM) {
+          L.sl_seg[nsl] = cur;
+          L.sl_k[nsl] = kst;
+        }
+        nsl++;
+      } else {
+        // (the list is full: no more speculation here; the lattice stops
+        // before this segment's first frame and the run decoder takes the
+        // rest, stores past it being undone as any others)
+        const uint64_t k0 = ka ? ka - 1 : 0;
+        if (tid == IO::CLAIM) __hip_atomic_fetch_max(P.lat + LW_BRK, ~k0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k0 < kst) {
+          stop = lat_rel(X0 + k0 * F, ss);
+          kst = k0;
+        }
+        quit = true;
+      }
+    }
+    if (quit && tid == IO::CLAIM) L.quit = 1;  // (read at the next segment's claim)
+    if constexpr (DT) {
+      // stores: each chunk XORed with the keys of the (at most two) frames it
+      // overlaps (a frame's header bytes get a zero mask), every chunk below
+      // the failing point known
+      const uint32_t xka = ka < kmax ? lat_rel(X0 + ka * F, ss) : 0xFFFFFFFFu;  // first lattice point (relative)
+      const uint32_t nent = brk != NONE32 ? 1u + brk : 1u + nl;
+      const uint32_t lo_r = lat_rel(P.lo, ss), hi_r = P.hi - ss < G::SEG ? (uint32_t)(P.hi - ss) : G::SEG;
+      const __amdgpu_buffer_rsrc_t rs = lat_rsrc(P, ss, G::SEG);
+      const bool any = !(P.opts & XYWS_OPT_NO_STORE);
+      const bool work = !(P.opts & XYWS_OPT_LATX_NOWORK);
+      uint32_t edge = 0;
+      u32x4 dprev = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (uint32_t k = 0; k < IO::K; k++) {
+        const bool ok = IO::valid(wave, k);
+        const uint32_t a = (ok ? IO::row(wave, k) : 0u) * 1024u + lane * 16u;
+        u32x4 d = *reinterpret_cast<const u32x4*>(&L.seg[a]);
+        uint32_t idx = 0;
+        if (a >= xka) {
+          const uint32_t dd = a - xka;
+          uint32_t qq = (uint32_t)((float)dd * rF);
+          if (qq * F32 > dd) qq--;
+          else if ((qq + 1) * F32 <= dd) qq++;
+          idx = 1 + qq;
+        }
+        if (work && idx < nent) d = d ^ lat_mask(L.tab, nent, idx, a);
+        const bool whole = ok && a >= lo_r && a + 16u <= hi_r && a + 16u <= stop;
+        if (ok && !whole && a < stop && a < hi_r && a + 16u > lo_r) {
+          edge |= 1u << k;
+          *reinterpret_cast<u32x4*>(&L.seg[a]) = d;  // (stored bytewise below)
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(d, rs, (whole && any) ? lane * 16u : OOB, IO::row(wave, k) * 1024u,
+                                               AUX_ST);
+        // (the store's data registers stay live past the next store)
+        asm volatile("" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
+        dprev = d;
+      }
+      asm volatile("s_nop 1" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
+      // chunks at the batch edges or at the failing point: their in-range
+      // bytes (XORed in LDS above; bytes at or past the failing point got a
+      // zero mask)
+#pragma nounroll
+      while (edge && any) {
+        const uint32_t k = __builtin_ctz(edge);
+        edge &= edge - 1;
+        const uint32_t a = IO::row(wave, k) * 1024u + lane * 16u;
+#pragma nounroll
+        for (uint32_t y = a; y < a + 16u; y++)
+          if (y >= lo_r && y < hi_r && y < stop) P.base[ss + y] = L.seg[y];
+      }
+      // descriptors of the segment's frames below the failing point (their
+      // headers from LDS: never XORed)
+      if (P.frames && stop && kst > ka) {
+        const uint32_t nd = (uint32_t)(kst - ka < nl ? kst - ka : nl);
+        for (uint32_t i = dl; i < nd; i += NDL) {
+          const uint64_t k = ka + i;
+          const uint64_t ord = L.c0 + k;
+          if (ord >= P.cap) break;
+          const uint64_t x = X0 + k * F;
+          const hdr_info h = lat_hdr(P, L.seg, (uint32_t)(x - ss), x);
+          if (h.hlen) write_frame(P, ord, x, h, x + h.hlen, 0);
+        }
+      }
+    }
+    it++;
+    // the control wave raises the decided prefix while the data waves store
+    if (clk.on && cl) clk.acc[LT_SEGS - 16]++;
+    cur = nxt;
+  }
+  clk.mark(cl ? LT_C_ADV : LT_D_ST);
+  clk.flush(P);
+  if (DT && tid == IO::CLAIM) L.nsl = nsl;  // (lat_check's list length)
+}
+
+// The end of a workgroup's work (whole workgroup): once every segment up to
+// its last speculative store has decided, the first failing point among them
+// is final for these stores; a store reaching past it (a segment stored
+// before the failing point was published) is undone: the same masks XORed
+// again over the same bytes (XOR is an involution), each frame's key from its
+// header in memory (headers are never written by a decode). Rare: a lattice
+// broken in the middle of a batch, after the first segments.
+template <class G>
+XYWS_DEV void lat_check(const run_params& P, lat_lds<G>& L, uint32_t tid) {
+  const uint32_t n = L.nsl & 0x7FFFFFFFu;
+  if (tid < 64 && n) {
+    lat_wait_decided(P, uniform64(L.E), L.sl_seg[n - 1], tid);
+    if (tid == 0) {
+      const uint64_t b = st_load(P.lat + LW_BRK);
+      L.kbf = b ? ~b : NONE;
+    }
+  }
+  __syncthreads();
+  if (!n) return;
+  const uint64_t kb = L.kbf, X0 = L.X0, F = L.F, kmax = L.kmax;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint64_t kst = L.sl_k[i];
+    if (kb == NONE || kb >= kst) continue;  // valid
+    const uint64_t ss = L.sl_seg[i] * G::SEG;
+    const uint64_t ka = ss <= X0 ? 0 : (ss - X0 + F - 1) / F;
+    const uint32_t stop = (uint32_t)(X0 + kst * F - ss < G::SEG ? X0 + kst * F - ss : G::SEG);
+    const uint32_t lo_r = lat_rel(P.lo, ss), hi_r = P.hi - ss < G::SEG ? (uint32_t)(P.hi - ss) : G::SEG;
+    const uint32_t top = stop < hi_r ? stop : hi_r;
+    for (uint32_t a = tid * 16u; a < top; a += G::NT * 16u) {
+      // the chunk's frames: g (at or before a) and g + 1, below kst
+      uint64_t g = a + ss < X0 ? NONE : (a + ss - X0) / F;  // (NONE: the carried frame)
+      u32x4 m = {0u, 0u, 0u, 0u};
+      for (int t = 0; t < 2; t++, g = g == NONE ? 0 : g + 1) {
+        uint4 en = {0u, 0u, 0u, 0u};
+        if (g == NONE) {
+          const cstate S0 = L.S0;
+          if (!(S0.st & S_NOCOV)) en = uint4{lat_rel(S0.cov_ps, ss), lat_rel(X0, ss), S0.cov_kw, 0u};
+        } else if (g < kst && g < kmax) {
+          const uint64_t x = X0 + g * F;
+          const hdr_info h = hdr_global(P, x, NONE);
+          if (h.hlen) {
+            const uint64_t ps = x + h.hlen;
+            const uint64_t end = g + 1 == kmax ? sat_add(ps, h.plen) : x + F;
+            en = uint4{lat_rel(ps, ss), lat_rel(end < P.hi ? end : P.hi, ss), aligned_key(h.key, ps, 0), 0u};
+          }
+        }
+        m.x |= en.z & range_mask32(a, en.x, en.y);
+        m.y |= en.z & range_mask32(a + 4, en.x, en.y);
+        m.z |= en.z & range_mask32(a + 8, en.x, en.y);
+        m.w |= en.z & range_mask32(a + 12, en.x, en.y);
+      }
+      (void)ka;
+#pragma unroll
+      for (uint32_t b = 0; b < 16; b++) {
+        const uint32_t y = a + b;
+        const uint32_t mw = b < 4 ? m.x : b < 8 ? m.y : b < 12 ? m.z : m.w;
+        const uint8_t kbyte = (uint8_t)(mw >> (8u * (b & 3u)));
+        if (kbyte && y >= lo_r && y < top) {
+          // (sc0 sc1: past this CU's L1, which may hold the bytes as loaded)
+          uint8_t* q = P.base + ss + y;
+          const uint8_t v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(q, (uint8_t)(v ^ kbyte), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+template <class G>
+__global__ void __launch_bounds__(G::NT)
+__attribute__((amdgpu_waves_per_eu(G::NT * G::WPC >= 256 ? G::NT * G::WPC / 256 : 1))) k_stream_lattice(run_params P) {
+  using IO = lat_io<G>;
   extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
   lat_lds<G>& L = *reinterpret_cast<lat_lds<G>*>(xs_lds);
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t tid = threadIdx.x;
   uint32_t* cnt = reinterpret_cast<uint32_t*>(P.lat + LW_CNT);
-  uint32_t ahead = NONE32;  // lane 0: the segment claimed one iteration ahead
-  if (tid == 0) {
+  uint32_t ahead = NONE32;  // claim lane: the segment claimed one iteration ahead
+  if (tid == IO::CLAIM) {
     L.E = st_load(P.lat + LW_EPOCH) + 1;
     const xyws_carry* cz = P.cin_user ? P.cin_user : &k_zero_carry;
     uint64_t c0 = 0;
@@ -294,6 +781,7 @@ __global__ void __launch_bounds__(G::NT, 1) k_stream_lattice(run_params P) {
     L.kmax = kmax;
     L.na = na;
     L.quit = 0;
+    L.nsl = 0;
     L.cur = NONE32;
     if (!na) {
       const uint32_t c = atomicAdd(cnt, 1u);
@@ -305,167 +793,21 @@ __global__ void __launch_bounds__(G::NT, 1) k_stream_lattice(run_params P) {
     }
   }
   __syncthreads();
-  const uint64_t E = uniform64(L.E);
   if (!L.na) {
-    const uint64_t X0 = uniform64(L.X0), F = uniform64(L.F), kmax = uniform64(L.kmax);
-    const float rF = 1.0f / (float)(F < (1ull << 24) ? F : (1ull << 24));
-    const uint32_t F32 = F < 0x80000000ull ? (uint32_t)F : 0x80000000u;
-    uint32_t cur = uniform32(L.cur);
-    u32x4 e[G::CH];
-    u32x4 epad = {0u, 0u, 0u, 0u};
-    auto issue = [&](uint32_t s) {
-      const __amdgpu_buffer_rsrc_t rs = lat_rsrc(P, (uint64_t)s * G::SEG, G::SEG + 16);
-#pragma unroll
-      for (uint32_t k = 0; k < G::CH; k++)
-        e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16u, k * G::NT * 16u, AUX_NT);
-      if (tid == 0) epad = __builtin_amdgcn_raw_buffer_load_b128(rs, 0u, G::SEG, AUX_NT);
-    };
-    if (cur != NONE32) issue(cur);
-    while (cur != NONE32) {
-      uint32_t t = tid;
-      asm volatile("" : "+v"(t));  // (lane address math per segment: see sweep_loop)
-      const uint64_t ss = (uint64_t)cur * G::SEG;
-      __syncthreads();  // the previous segment's LDS reads are done
-#pragma unroll
-      for (uint32_t k = 0; k < G::CH; k++) *reinterpret_cast<u32x4*>(&L.seg[(k * G::NT + t) * 16u]) = e[k];
-      if (t == 0) {
-        *reinterpret_cast<u32x4*>(&L.seg[G::SEG]) = epad;
-        L.nxt = ahead;
-        if (ahead != NONE32) {
-          if (L.quit) {
-            ahead = NONE32;
-          } else {
-            const uint32_t a = atomicAdd(cnt, 1u);
-            ahead = a < P.nseg ? a : NONE32;
-          }
-        }
-        L.brk = NONE32;
-      }
-      __syncthreads();
-      const uint32_t nxt = uniform32(L.nxt);
-      if (nxt != NONE32) issue(nxt);  // (in flight through the checks, the look-back and the stores)
-      // lattice points in the segment: k in [ka, kz)
-      const uint64_t se = ss + G::SEG;
-      const uint64_t ka = ss <= X0 ? 0 : (ss - X0 + F - 1) / F;
-      uint64_t kz = se <= X0 ? 0 : (se - X0 + F - 1) / F;
-      if (kz > kmax) kz = kmax;
-      const uint32_t nl = kz > ka ? (uint32_t)(kz - ka) : 0u;
-      const uint32_t xka = ka < kmax ? lat_rel(X0 + ka * F, ss) : 0xFFFFFFFFu;  // first lattice point (relative)
-      // entry 0: the frame covering the segment's first bytes
-      if (t == G::NT - 1) {
-        uint4 c = {0u, 0u, 0u, 0u};
-        if (ka == 0) {
-          const cstate S0 = L.S0;
-          if (!(S0.st & S_NOCOV)) c = uint4{lat_rel(S0.cov_ps, ss), lat_rel(X0, ss), S0.cov_kw, 0u};
-        } else {
-          const uint64_t xc = X0 + (ka - 1) * F;
-          const hdr_info h = hdr_global(P, xc, NONE);
-          if (h.hlen) {
-            const uint64_t ps = xc + h.hlen;
-            const uint64_t end = ka - 1 + 1 == kmax ? sat_add(ps, h.plen) : xc + F;
-            c = uint4{lat_rel(ps, ss), lat_rel(end < P.hi ? end : P.hi, ss), aligned_key(h.key, ps, 0), 0u};
-          }
-        }
-        L.tab[0] = c;
-      }
-      // entries 1..nl: the lattice points, each checked by one lane
-      for (uint32_t i = t; i < nl; i += G::NT) {
-        const uint64_t k = ka + i;
-        const uint64_t x = X0 + k * F;
-        const uint32_t xr = (uint32_t)(x - ss);
-        const hdr_info h = lat_hdr(P, L.seg, xr, x);
-        const bool last = k + 1 == kmax;
-        const uint64_t fend = h.hlen ? sat_add(x + h.hlen, h.plen) : x;
-        // the point holds: a frame of exactly F bytes, or the batch's last
-        // frame (cut by the batch end, or a header the end cuts)
-        const bool ok = h.hlen ? ((uint64_t)h.hlen + h.plen == F && h.plen < F) || (last && fend >= P.hi) : last;
-        if (!ok) atomicMin(&L.brk, i);
-        uint4 en = {xr, xr, 0u, 0u};
-        if (h.hlen) {
-          const uint64_t ps = x + h.hlen;
-          en = uint4{lat_rel(ps, ss), lat_rel(fend < P.hi ? fend : P.hi, ss), aligned_key(h.key, ps, 0), 0u};
-        }
-        L.tab[1 + i] = en;
-      }
-      __syncthreads();
-      const uint32_t brk = uniform32(L.brk);
-      if (t == 0) {
-        if (brk != NONE32)
-          __hip_atomic_fetch_max(P.lat + LW_BRK, ~(ka + brk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        st_store(P.lat + LW_STAT + cur, (E << 2) | (brk != NONE32 ? LS_BRK : LS_AGG));
-      }
-      if (t < 64) {
-        const int go = lat_lookback(P, cur, E, ka, lane);
-        if (t == 0) {
-          L.go = (uint32_t)go;
-          if (go && brk == NONE32) st_store(P.lat + LW_STAT + cur, (E << 2) | LS_INCL);
-          if (!go || brk != NONE32) L.quit = 1;  // the rest of the batch is the run decoder's
-        }
-      }
-      __syncthreads();
-      // stores: every chunk below the first failing point (nothing when an
-      // earlier point failed); entries past it are left out
-      const uint32_t go = uniform32(L.go);
-      const uint32_t nent = brk != NONE32 ? 1u + brk : 1u + nl;
-      const uint32_t stop = !go ? 0u : brk != NONE32 ? (uint32_t)(X0 + (ka + brk) * F - ss) : G::SEG;
-      const uint32_t lo_r = lat_rel(P.lo, ss), hi_r = P.hi - ss < G::SEG ? (uint32_t)(P.hi - ss) : G::SEG;
-      const __amdgpu_buffer_rsrc_t rs = lat_rsrc(P, ss, G::SEG);
-      const bool any = !(P.opts & XYWS_OPT_NO_STORE);
-      u32x4 dprev = {0u, 0u, 0u, 0u};
-      uint32_t edge = 0;
-#pragma unroll
-      for (uint32_t k = 0; k < G::CH; k++) {
-        const uint32_t a = (k * G::NT + t) * 16u;
-        uint32_t idx = 0;
-        if (a >= xka) {
-          const uint32_t d = a - xka;
-          uint32_t qq = (uint32_t)((float)d * rF);
-          if (qq * F32 > d) qq--;
-          else if ((qq + 1) * F32 <= d) qq++;
-          idx = 1 + qq;
-        }
-        const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
-        const u32x4 m = idx < nent ? lat_mask(L.tab, nent, idx, a) : u32x4{0u, 0u, 0u, 0u};
-        const bool whole = a >= lo_r && a + 16u <= hi_r && a + 16u <= stop;
-        if (!whole && a < stop && a < hi_r && a + 16u > lo_r) edge |= 1u << k;
-        const u32x4 d = v ^ m;
-        __builtin_amdgcn_raw_buffer_store_b128(d, rs, (whole && any) ? t * 16u : OOB, k * G::NT * 16u, AUX_ST);
-        asm volatile("" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
-        dprev = d;
-      }
-      asm volatile("s_nop 1" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
-      // chunks at the batch edges or at the failing point: their in-range bytes
-#pragma nounroll
-      while (edge && any) {
-        const uint32_t k = __builtin_ctz(edge);
-        edge &= edge - 1;
-        const uint32_t a = (k * G::NT + t) * 16u;
-        uint32_t idx = 0;
-        if (a >= xka) idx = 1 + (a - xka) / F32;
-        if (idx >= nent) continue;
-        const u32x4 m = lat_mask(L.tab, nent, idx, a);
-#pragma nounroll
-        for (uint32_t b = 0; b < 16; b++) {
-          const uint32_t y = a + b;
-          const uint32_t mw = b < 4 ? m.x : b < 8 ? m.y : b < 12 ? m.z : m.w;
-          const uint8_t kb = (uint8_t)(mw >> (8u * (b & 3u)));
-          if (kb && y >= lo_r && y < hi_r && y < stop) P.base[ss + y] = L.seg[y] ^ kb;
-        }
-      }
-      // descriptors of the segment's frames below the failing point
-      if (P.frames && go) {
-        const uint32_t nd = brk != NONE32 ? brk : nl;
-        for (uint32_t i = t; i < nd; i += G::NT) {
-          const uint64_t k = ka + i;
-          const uint64_t ord = L.c0 + k;
-          if (ord >= P.cap) break;
-          const uint64_t x = X0 + k * F;
-          const hdr_info h = lat_hdr(P, L.seg, (uint32_t)(x - ss), x);
-          if (h.hlen) write_frame(P, ord, x, h, x + h.hlen, 0);
-        }
-      }
-      cur = nxt;
+    if constexpr (IO::CTRL) {
+      // (a wave-uniform branch: each loop is a scalar branch target)
+      if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0)
+        lat_loop<G, LR_CTRL>(P, L, tid, ahead);
+      else
+        lat_loop<G, LR_DATA>(P, L, tid, ahead);
+    } else {
+      lat_loop<G, LR_ALL>(P, L, tid, ahead);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint64_t te = stats_on(P) && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
+    lat_check<G>(P, L, tid);
+    if (te) stat_add(P, LT_END, __builtin_amdgcn_s_memtime() - te);  // (stats: the end-of-work check)
   }
   // end of the workgroup: the last one to finish writes the call's outputs
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -481,6 +823,10 @@ __global__ void __launch_bounds__(G::NT, 1) k_stream_lattice(run_params P) {
     L.done_last = last;
   }
   __syncthreads();
-  if (!L.done_last || tid != 0) return;
+  if (!L.done_last) return;
+  // (the last workgroup: the group counters back to zero for the next call)
+  for (uint64_t g = tid; g * LAT_GRP < P.nseg; g += G::NT)
+    __hip_atomic_store(P.lgrp + g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid != 0) return;
   lat_finish<G>(P, L);
 }

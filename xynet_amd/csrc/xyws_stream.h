@@ -70,6 +70,11 @@ int stream_scratch_unmask_counter(stream_scratch* s, bool capturing, uint32_t** 
 #define XYWS_OPT_RUNS 0x80000000u     // the run decoder, whatever the decoder choice would take
 #define XYWS_OPT_LATTICE 0x400u      // the lattice decoder first, whatever the decoder choice would take
 #define XYWS_OPT_NO_LATDEC 0x800u    // never the lattice decoder
+#define XYWS_OPT_TEST_LATSPEC 0x10u  // tests (lattice decoder): every store speculative (no first-segment gate, no
+                                     // failing-point filter): a broken lattice is undone by the end-of-work check
+#define XYWS_OPT_LATX_2WG 0x20u  // experiment (lattice decoder): the two-workgroups-per-CU geometry (G_LAT2)
+#define XYWS_OPT_LATX_NOWORK 0x40u  // timing experiment only (wrong bytes): the lattice decoder's data waves skip
+                                    // the checks and the XOR (its data path and control alone)
 #define XYWS_OPT_REDIRECT 0x2000u    // (set by stream_decode_fused only) the run decoder after the lattice decoder:
                                      // it reads the lattice's redirect record first
 #define XYWS_OPT_TEST_SPEC 0x2000000u  // tests (sweep decoder): segments 1, 4, 7, ... report no entry, segments

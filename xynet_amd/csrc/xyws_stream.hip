@@ -276,6 +276,7 @@ struct run_params {
   // redirected batch (counts and ordinals go on from there) and the offset of
   // its start in the caller's batch (descriptor offsets)
   uint64_t* lat;
+  uint64_t* lgrp;  // lattice decoder: decided-segment counts per LAT_GRP segments
   uint32_t segb;
   uint64_t tbias, obias;
 };
@@ -4246,7 +4247,7 @@ static int lat_grow(stream_scratch* s, uint64_t segs, bool capturing) {
   if (s->lmem && segs <= s->lmax_segs) return XYWS_OK;
   if (capturing) return XYWS_ERR_CAPACITY;
   const uint64_t want = segs < 64 ? 64 : segs;
-  const uint64_t bytes = 8 * (LW_STAT + want);
+  const uint64_t bytes = 8 * (LW_STAT + want + want / LAT_GRP + 1);  // (statuses, then group counts)
   void* m = nullptr;
   if (hipMalloc(&m, bytes) != hipSuccess) return XYWS_ERR_NOMEM;
   if (s->lmem) {
@@ -4356,7 +4357,9 @@ static bool lattice_preferred(const stream_scratch* s) {
   if (!s->pol_h) return false;
   const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
   if (!s->pol_h[0]) return true;  // (no call has finished on this stream)
-  return fsmax && fsmin == fsmax && fsmin >= LAT_FMIN;
+  // (equal frames of up to LAT_FAUTO bytes: above it the sweep decoder is
+  // faster today)
+  return fsmax && fsmin == fsmax && fsmin >= LAT_FMIN && fsmax <= LAT_FAUTO;
 }
 
 template <class G>
@@ -4500,15 +4503,19 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   }
   if (want_lat) {
     // the lattice decoder first; the run decoder after it reads its redirect record
-    const uint64_t lseg = small ? G_LAT_SMALL::SEG : G_LAT::SEG;
+    const bool two = !small && (opts & XYWS_OPT_LATX_2WG);
+    const uint64_t lseg = small ? G_LAT_SMALL::SEG : two ? G_LAT2::SEG : G_LAT::SEG;
     const uint64_t lnseg = (hi + lseg - 1) / lseg;
     if (const int rc = lat_grow(s, lnseg, cs != hipStreamCaptureStatusNone)) return rc;
     run_params PL = P;
     PL.lat = static_cast<uint64_t*>(s->lmem);
+    PL.lgrp = PL.lat + LW_STAT + s->lmax_segs;
     PL.nseg = lnseg;
-    const uint64_t maxg = small ? 64 : (uint64_t)s->ncu;
+    const uint64_t maxg = small ? 64 : (uint64_t)s->ncu * (two ? G_LAT2::WPC : G_LAT::WPC);
     const uint32_t grid = (uint32_t)(lnseg < maxg ? lnseg : maxg);
-    const int rc = small ? launch_lattice<G_LAT_SMALL>(PL, grid, stream) : launch_lattice<G_LAT>(PL, grid, stream);
+    const int rc = small ? launch_lattice<G_LAT_SMALL>(PL, grid, stream)
+                   : two ? launch_lattice<G_LAT2>(PL, grid, stream)
+                         : launch_lattice<G_LAT>(PL, grid, stream);
     if (rc) return rc;
     P.lat = PL.lat;
     P.opts |= XYWS_OPT_REDIRECT;
