@@ -167,7 +167,7 @@ def test_lattice_then_irregular_then_lattice(ws, oracle):
     the run decoder once more (the choice follows the previous call), then the
     lattice again (policy word 4: 3 = lattice)."""
     dec = ws.frame_decoder()
-    reg = regular(1, 256, 8000)  # (equal frames of up to LAT_FAUTO bytes)
+    reg = regular(1, 4096, 500)
     irr = streams.case_bytes("random_frames_300")
     used = []
     for src in (reg, reg, irr, irr, reg, reg):

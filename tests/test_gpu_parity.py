@@ -299,7 +299,8 @@ def test_lattice_entry_follows_the_previous_call(ws, oracle):
     for src in (bytes(regular), bytes(regular), bytes(fakes), bytes(other)):
         # (a new decoder per batch: a fresh carry; the policy words belong to
         # the stream's scratch and stay)
-        dec = ws.frame_decoder(opts=_lib.OPT_STATS)
+        # (the run decoder itself: equal small frames would take the lattice decoder)
+        dec = ws.frame_decoder(opts=_lib.OPT_STATS | _lib.OPT_NO_LATDEC)
         view, _ = dev_bytes(src)
         ob = np.frombuffer(src, np.uint8).copy()
         ofr, carry, on = oracle.decode_stream(ob, cap=len(src) // 8 + 2)

@@ -47,7 +47,6 @@
 
 constexpr uint64_t LAT_FMIN = 128;          // smaller frames: the run decoder (its dense pass)
 constexpr uint64_t LAT_FMAX = 1ull << 40;   // (lattice arithmetic stays well inside 64 bits)
-constexpr uint64_t LAT_FAUTO = 1024;        // the decoder choice takes the lattice for equal frames up to this size
 // lattice scratch (u64 words, zeroed at allocation)
 enum {
   LW_CNT = 0,      // u32 [0] claim counter, u32 [1] done count (reset by the finisher)
@@ -341,6 +340,25 @@ XYWS_DEV uint64_t lat_load_late(const uint64_t* p) {
   return v;
 }
 
+// LW_BRK and its replicas (P.lbrk: LAT_NREP words LAT_REPW apart, each
+// workgroup reading one per segment: one word read by every CU at the
+// coherence point each segment cost a third of the bandwidth,
+// scripts/bw_probe9). Raised (wave 0, every lane) to failing point k: the
+// word itself with a returning atomic, then every replica, all completed
+// before the caller publishes anything.
+constexpr uint32_t LAT_NREP = 64, LAT_REPW = 32;
+// (word offset of the replicas in the lattice scratch: after the statuses and
+// the group counts, 256-byte aligned)
+inline constexpr uint64_t lat_rep_off(uint64_t segs) {
+  return (LW_STAT + segs + segs / 64 + 1 + LAT_REPW - 1) / LAT_REPW * LAT_REPW;
+}
+XYWS_DEV void lat_raise_brk(const run_params& P, uint64_t k, uint32_t lane) {
+  uint64_t o = 0;
+  if (lane == 0) o = __hip_atomic_fetch_max(P.lat + LW_BRK, ~k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_max(P.lbrk + LAT_REPW * lane, ~k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(o)::"memory");
+}
+
 // The claim wave's extra loads for segment s, one dword per lane, issued with
 // its rows: lanes 0..3 the 16 bytes after the segment, lanes 4..8 the 20
 // bytes at the dword at or below the header of the frame covering the
@@ -559,12 +577,8 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
     const bool gate = it == 0 && !blind;
     if (CT && tid < 64) {
       // the segment's own result, published while the data waves store
+      if (brk != NONE32) lat_raise_brk(P, ka + brk, lane);  // (completed before the result is published)
       if (tid == 0) {
-        // (a returning atomic, its value used: performed before the result is published)
-        if (brk != NONE32) {
-          uint64_t o = __hip_atomic_fetch_max(P.lat + LW_BRK, ~(ka + brk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          asm volatile("s_waitcnt vmcnt(0)" : "+v"(o)::"memory");
-        }
         st_store(P.lat + LW_STAT + cur, (E << 2) | (brk != NONE32 ? LS_BRK : LS_AGG));
         __hip_atomic_fetch_add(P.lgrp + cur / LAT_GRP, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -574,7 +588,7 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
       }
       // the load for the next segment's decision (the last operation of the
       // phase: used a segment later)
-      if (tid == 0) brk_seen = lat_load_late(P.lat + LW_BRK);
+      if (tid == 0) brk_seen = lat_load_late(P.lbrk + LAT_REPW * (blockIdx.x % LAT_NREP));
     }
     if (gate) __syncthreads();  // (D, the first segment only) the fresh failing point
     clk.mark(cl ? LT_C_C : LT_D_WD);
@@ -599,7 +613,10 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
         // before this segment's first frame and the run decoder takes the
         // rest, stores past it being undone as any others)
         const uint64_t k0 = ka ? ka - 1 : 0;
-        if (tid == IO::CLAIM) __hip_atomic_fetch_max(P.lat + LW_BRK, ~k0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == IO::CLAIM)
+          for (uint32_t r = 0; r <= LAT_NREP; r++)
+            __hip_atomic_fetch_max(r < LAT_NREP ? P.lbrk + LAT_REPW * r : P.lat + LW_BRK, ~k0, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         if (k0 < kst) {
           stop = lat_rel(X0 + k0 * F, ss);
           kst = k0;
@@ -827,6 +844,7 @@ __attribute__((amdgpu_waves_per_eu(G::NT * G::WPC >= 256 ? G::NT * G::WPC / 256 
   // (the last workgroup: the group counters back to zero for the next call)
   for (uint64_t g = tid; g * LAT_GRP < P.nseg; g += G::NT)
     __hip_atomic_store(P.lgrp + g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid < LAT_NREP) __hip_atomic_store(P.lbrk + LAT_REPW * tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid != 0) return;
   lat_finish<G>(P, L);
 }

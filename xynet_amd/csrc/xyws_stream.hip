@@ -277,6 +277,7 @@ struct run_params {
   // its start in the caller's batch (descriptor offsets)
   uint64_t* lat;
   uint64_t* lgrp;  // lattice decoder: decided-segment counts per LAT_GRP segments
+  uint64_t* lbrk;  // lattice decoder: the replicas of LW_BRK
   uint32_t segb;
   uint64_t tbias, obias;
 };
@@ -4247,7 +4248,7 @@ static int lat_grow(stream_scratch* s, uint64_t segs, bool capturing) {
   if (s->lmem && segs <= s->lmax_segs) return XYWS_OK;
   if (capturing) return XYWS_ERR_CAPACITY;
   const uint64_t want = segs < 64 ? 64 : segs;
-  const uint64_t bytes = 8 * (LW_STAT + want + want / LAT_GRP + 1);  // (statuses, then group counts)
+  const uint64_t bytes = 8 * (lat_rep_off(want) + LAT_NREP * LAT_REPW);  // (statuses, group counts, LW_BRK replicas)
   void* m = nullptr;
   if (hipMalloc(&m, bytes) != hipSuccess) return XYWS_ERR_NOMEM;
   if (s->lmem) {
@@ -4357,9 +4358,7 @@ static bool lattice_preferred(const stream_scratch* s) {
   if (!s->pol_h) return false;
   const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
   if (!s->pol_h[0]) return true;  // (no call has finished on this stream)
-  // (equal frames of up to LAT_FAUTO bytes: above it the sweep decoder is
-  // faster today)
-  return fsmax && fsmin == fsmax && fsmin >= LAT_FMIN && fsmax <= LAT_FAUTO;
+  return fsmax && fsmin == fsmax && fsmin >= LAT_FMIN;
 }
 
 template <class G>
@@ -4510,6 +4509,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     run_params PL = P;
     PL.lat = static_cast<uint64_t*>(s->lmem);
     PL.lgrp = PL.lat + LW_STAT + s->lmax_segs;
+    PL.lbrk = PL.lat + lat_rep_off(s->lmax_segs);
     PL.nseg = lnseg;
     const uint64_t maxg = small ? 64 : (uint64_t)s->ncu * (two ? G_LAT2::WPC : G_LAT::WPC);
     const uint32_t grid = (uint32_t)(lnseg < maxg ? lnseg : maxg);
