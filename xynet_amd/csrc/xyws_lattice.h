@@ -59,7 +59,8 @@ enum {
   LW_STAT = 32     // per segment: (E << 2) | LS_*
 };
 enum { LS_AGG = 1, LS_BRK = 3 };
-constexpr uint32_t LAT_SLIST = 512;  // speculative stores a workgroup records for its end-of-work check
+constexpr uint32_t LAT_SLIST = 512;
+constexpr uint32_t LAT_NOCLAIM = 0x7FFFFFFFu;  // (no claim: the next segment after it is none)  // speculative stores a workgroup records for its end-of-work check
 enum : uint64_t { RD_DONE = 0, RD_FULL = 1, RD_FROM = 2 };
 
 template <uint32_t NT_, uint32_t SEG_, uint32_t WPC_ = 1>
@@ -352,6 +353,7 @@ constexpr uint32_t LAT_NREP = 64, LAT_REPW = 32;
 inline constexpr uint64_t lat_rep_off(uint64_t segs) {
   return (LW_STAT + segs + segs / 64 + 1 + LAT_REPW - 1) / LAT_REPW * LAT_REPW;
 }
+inline constexpr uint64_t lat_sl_off(uint64_t segs) { return lat_rep_off(segs) + LAT_NREP * LAT_REPW; }
 XYWS_DEV void lat_raise_brk(const run_params& P, uint64_t k, uint32_t lane) {
   uint64_t o = 0;
   if (lane == 0) o = __hip_atomic_fetch_max(P.lat + LW_BRK, ~k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -449,7 +451,7 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
           if (claim)
             asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(ahead) : "v"(cnt), "v"(1u) : "memory");
           else
-            ahead = NONE32;
+            ahead = LAT_NOCLAIM;
         }
         cx = lat_ctrl_load(P, s, G::SEG, X0, F, kmax, tid);
       }
@@ -496,7 +498,9 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
       const uint32_t ln = tid & 63u;  // (from the per-segment opaque tid: not hoisted)
       if (ln < 9) *reinterpret_cast<uint32_t*>(&L.seg[G::SEG + 4u * ln]) = cx;
       if (lane == 0) {
-        L.nxt = ahead < P.nseg ? ahead : NONE32;  // (claimed a segment ago)
+        // (claimed a segment ago: the counter's value, after the static first round)
+        const uint32_t a = ahead + 2u * gridDim.x;  // (LAT_NOCLAIM: past every segment)
+        L.nxt = a < P.nseg ? a : NONE32;
         L.brk = NONE32;
       }
     }
@@ -699,74 +703,73 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
   if (DT && tid == IO::CLAIM) L.nsl = nsl;  // (lat_check's list length)
 }
 
-// The end of a workgroup's work (whole workgroup): once every segment up to
-// its last speculative store has decided, the first failing point among them
-// is final for these stores; a store reaching past it (a segment stored
-// before the failing point was published) is undone: the same masks XORed
-// again over the same bytes (XOR is an involution), each frame's key from its
-// header in memory (headers are never written by a decode). Rare: a lattice
-// broken in the middle of a batch, after the first segments.
+// Speculative stores (lat_loop): a workgroup's list of the segments it stored
+// before every earlier one had decided, and the lattice index each segment's
+// stores stop at, goes to its slice of P.lsl when its work ends (n, then
+// {segment, index} pairs; LAT_LSW words per workgroup).
+constexpr uint32_t LAT_LSW = 1 + 2 * LAT_SLIST;
 template <class G>
-XYWS_DEV void lat_check(const run_params& P, lat_lds<G>& L, uint32_t tid) {
-  const uint32_t n = L.nsl & 0x7FFFFFFFu;
-  if (tid < 64 && n) {
-    lat_wait_decided(P, uniform64(L.E), L.sl_seg[n - 1], tid);
-    if (tid == 0) {
-      const uint64_t b = st_load(P.lat + LW_BRK);
-      L.kbf = b ? ~b : NONE;
-    }
+XYWS_DEV void lat_dump_list(const run_params& P, const lat_lds<G>& L, uint32_t tid) {
+  const uint32_t n = L.nsl;
+  uint64_t* q = P.lsl + (uint64_t)blockIdx.x * LAT_LSW;
+  if (tid == 0) q[0] = n;
+  for (uint32_t i = tid; i < n; i += G::NT) {
+    q[1 + 2 * i] = L.sl_seg[i];
+    q[2 + 2 * i] = L.sl_k[i];
   }
-  __syncthreads();
-  if (!n) return;
-  const uint64_t kb = L.kbf, X0 = L.X0, F = L.F, kmax = L.kmax;
-  for (uint32_t i = 0; i < n; i++) {
-    const uint64_t kst = L.sl_k[i];
-    if (kb == NONE || kb >= kst) continue;  // valid
-    const uint64_t ss = L.sl_seg[i] * G::SEG;
-    const uint64_t ka = ss <= X0 ? 0 : (ss - X0 + F - 1) / F;
-    const uint32_t stop = (uint32_t)(X0 + kst * F - ss < G::SEG ? X0 + kst * F - ss : G::SEG);
-    const uint32_t lo_r = lat_rel(P.lo, ss), hi_r = P.hi - ss < G::SEG ? (uint32_t)(P.hi - ss) : G::SEG;
-    const uint32_t top = stop < hi_r ? stop : hi_r;
-    for (uint32_t a = tid * 16u; a < top; a += G::NT * 16u) {
-      // the chunk's frames: g (at or before a) and g + 1, below kst
-      uint64_t g = a + ss < X0 ? NONE : (a + ss - X0) / F;  // (NONE: the carried frame)
-      u32x4 m = {0u, 0u, 0u, 0u};
-      for (int t = 0; t < 2; t++, g = g == NONE ? 0 : g + 1) {
-        uint4 en = {0u, 0u, 0u, 0u};
-        if (g == NONE) {
-          const cstate S0 = L.S0;
-          if (!(S0.st & S_NOCOV)) en = uint4{lat_rel(S0.cov_ps, ss), lat_rel(X0, ss), S0.cov_kw, 0u};
-        } else if (g < kst && g < kmax) {
-          const uint64_t x = X0 + g * F;
-          const hdr_info h = hdr_global(P, x, NONE);
-          if (h.hlen) {
-            const uint64_t ps = x + h.hlen;
-            const uint64_t end = g + 1 == kmax ? sat_add(ps, h.plen) : x + F;
-            en = uint4{lat_rel(ps, ss), lat_rel(end < P.hi ? end : P.hi, ss), aligned_key(h.key, ps, 0), 0u};
-          }
+}
+
+// The undo of segment s's stores past the final failing point kb (whole
+// workgroup; the finisher, every workgroup done): the stores reached lattice
+// index kst > kb (the segment stored before the failing point was
+// published); the bytes from X0 + kb*F to where they stopped get the same
+// masks again (XOR is an involution), each frame's key from its header in
+// memory (headers are never written by a decode). Rare: a lattice broken in
+// the middle of a batch, after the first segments.
+template <class G>
+XYWS_DEV void lat_undo(const run_params& P, const lat_lds<G>& L, uint32_t tid, uint64_t s, uint64_t kst, uint64_t kb) {
+  const uint64_t X0 = L.X0, F = L.F, kmax = L.kmax;
+  const uint64_t ss = s * G::SEG;
+  const uint32_t stop = (uint32_t)(X0 + kst * F - ss < G::SEG ? X0 + kst * F - ss : G::SEG);
+  const uint32_t lo_r = lat_rel(P.lo, ss), hi_r = P.hi - ss < G::SEG ? (uint32_t)(P.hi - ss) : G::SEG;
+  const uint32_t top = stop < hi_r ? stop : hi_r;
+  const uint32_t from = lat_rel(X0 + kb * F, ss);  // (the run decoder's bytes: decoded again from there)
+  for (uint32_t a = (from & ~15u) + tid * 16u; a < top; a += G::NT * 16u) {
+    // the chunk's frames: g (at or before a) and g + 1, below kst
+    uint64_t g = a + ss < X0 ? NONE : (a + ss - X0) / F;  // (NONE: the carried frame)
+    u32x4 m = {0u, 0u, 0u, 0u};
+    for (int t = 0; t < 2; t++, g = g == NONE ? 0 : g + 1) {
+      uint4 en = {0u, 0u, 0u, 0u};
+      if (g == NONE) {
+        const cstate S0 = L.S0;
+        if (!(S0.st & S_NOCOV)) en = uint4{lat_rel(S0.cov_ps, ss), lat_rel(X0, ss), S0.cov_kw, 0u};
+      } else if (g < kst && g < kmax) {
+        const uint64_t x = X0 + g * F;
+        const hdr_info h = hdr_global(P, x, NONE);
+        if (h.hlen) {
+          const uint64_t ps = x + h.hlen;
+          const uint64_t end = g + 1 == kmax ? sat_add(ps, h.plen) : x + F;
+          en = uint4{lat_rel(ps, ss), lat_rel(end < P.hi ? end : P.hi, ss), aligned_key(h.key, ps, 0), 0u};
         }
-        m.x |= en.z & range_mask32(a, en.x, en.y);
-        m.y |= en.z & range_mask32(a + 4, en.x, en.y);
-        m.z |= en.z & range_mask32(a + 8, en.x, en.y);
-        m.w |= en.z & range_mask32(a + 12, en.x, en.y);
       }
-      (void)ka;
+      m.x |= en.z & range_mask32(a, en.x, en.y);
+      m.y |= en.z & range_mask32(a + 4, en.x, en.y);
+      m.z |= en.z & range_mask32(a + 8, en.x, en.y);
+      m.w |= en.z & range_mask32(a + 12, en.x, en.y);
+    }
 #pragma unroll
-      for (uint32_t b = 0; b < 16; b++) {
-        const uint32_t y = a + b;
-        const uint32_t mw = b < 4 ? m.x : b < 8 ? m.y : b < 12 ? m.z : m.w;
-        const uint8_t kbyte = (uint8_t)(mw >> (8u * (b & 3u)));
-        if (kbyte && y >= lo_r && y < top) {
-          // (sc0 sc1: past this CU's L1, which may hold the bytes as loaded)
-          uint8_t* q = P.base + ss + y;
-          const uint8_t v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(q, (uint8_t)(v ^ kbyte), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    for (uint32_t b = 0; b < 16; b++) {
+      const uint32_t y = a + b;
+      const uint32_t mw = b < 4 ? m.x : b < 8 ? m.y : b < 12 ? m.z : m.w;
+      const uint8_t kbyte = (uint8_t)(mw >> (8u * (b & 3u)));
+      if (kbyte && y >= from && y >= lo_r && y < top) {
+        // (agent scope: past this CU's caches, which may hold the bytes as loaded)
+        uint8_t* q = P.base + ss + y;
+        const uint8_t v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(q, (uint8_t)(v ^ kbyte), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
 }
 
 template <class G>
@@ -801,12 +804,12 @@ __attribute__((amdgpu_waves_per_eu(G::NT * G::WPC >= 256 ? G::NT * G::WPC / 256 
     L.nsl = 0;
     L.cur = NONE32;
     if (!na) {
-      const uint32_t c = atomicAdd(cnt, 1u);
-      if (c < P.nseg) {
-        L.cur = c;
-        const uint32_t a = atomicAdd(cnt, 1u);
-        ahead = a < P.nseg ? a : NONE32;
-      }
+      // the first round is static (segment b, then b + grid: every
+      // workgroup's first segment, the one its gate holds, is among the
+      // first grid segments, so no gate waits on a segment that waits itself),
+      // then claims from the counter offset by 2 * grid (lat_loop)
+      L.cur = blockIdx.x < P.nseg ? blockIdx.x : NONE32;
+      ahead = blockIdx.x - gridDim.x;  // (+ 2 * grid at its use: b + grid)
     }
   }
   __syncthreads();
@@ -820,11 +823,8 @@ __attribute__((amdgpu_waves_per_eu(G::NT * G::WPC >= 256 ? G::NT * G::WPC / 256 
     } else {
       lat_loop<G, LR_ALL>(P, L, tid, ahead);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const uint64_t te = stats_on(P) && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
-    lat_check<G>(P, L, tid);
-    if (te) stat_add(P, LT_END, __builtin_amdgcn_s_memtime() - te);  // (stats: the end-of-work check)
+    lat_dump_list<G>(P, L, tid);
   }
   // end of the workgroup: the last one to finish writes the call's outputs
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -841,7 +841,27 @@ __attribute__((amdgpu_waves_per_eu(G::NT * G::WPC >= 256 ? G::NT * G::WPC / 256 
   }
   __syncthreads();
   if (!L.done_last) return;
-  // (the last workgroup: the group counters back to zero for the next call)
+  // the last workgroup: every segment has decided, LW_BRK is final; stores
+  // past it are undone (every workgroup's list)
+  if (tid == 0) {
+    const uint64_t b = st_load(P.lat + LW_BRK);
+    L.kbf = b && !L.na ? ~b : NONE;
+  }
+  __syncthreads();
+  const uint64_t kb = L.kbf;
+  if (kb != NONE) {
+    for (uint32_t w = 0; w < gridDim.x; w++) {
+      const uint64_t* q = P.lsl + (uint64_t)w * LAT_LSW;
+      const uint32_t n = (uint32_t)st_load(q);
+      for (uint32_t i = 0; i < n; i++) {
+        const uint64_t kst = st_load(q + 2 + 2 * i);
+        if (kb < kst) lat_undo<G>(P, L, tid, st_load(q + 1 + 2 * i), kst, kb);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // (the group counters back to zero for the next call)
   for (uint64_t g = tid; g * LAT_GRP < P.nseg; g += G::NT)
     __hip_atomic_store(P.lgrp + g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid < LAT_NREP) __hip_atomic_store(P.lbrk + LAT_REPW * tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -278,6 +278,7 @@ struct run_params {
   uint64_t* lat;
   uint64_t* lgrp;  // lattice decoder: decided-segment counts per LAT_GRP segments
   uint64_t* lbrk;  // lattice decoder: the replicas of LW_BRK
+  uint64_t* lsl;   // lattice decoder: the workgroups' speculative-store lists (LAT_LSW words each)
   uint32_t segb;
   uint64_t tbias, obias;
 };
@@ -4244,11 +4245,16 @@ static int sweep_grow(stream_scratch* s, uint64_t segs, bool capturing) {
 // Lattice decoder scratch for up to `segs` segments: LW_STAT words of
 // scratch and one result word per segment, all zeroed at allocation (epoch 0:
 // no result of any call).
+static uint64_t lat_max_grid(const stream_scratch* s) {
+  const uint64_t g = (uint64_t)s->ncu * 2;  // (G_LAT2: two workgroups per CU)
+  return g > 64 ? g : 64;
+}
 static int lat_grow(stream_scratch* s, uint64_t segs, bool capturing) {
   if (s->lmem && segs <= s->lmax_segs) return XYWS_OK;
   if (capturing) return XYWS_ERR_CAPACITY;
   const uint64_t want = segs < 64 ? 64 : segs;
-  const uint64_t bytes = 8 * (lat_rep_off(want) + LAT_NREP * LAT_REPW);  // (statuses, group counts, LW_BRK replicas)
+  // (statuses, group counts, LW_BRK replicas, one list per workgroup)
+  const uint64_t bytes = 8 * (lat_sl_off(want) + lat_max_grid(s) * LAT_LSW);
   void* m = nullptr;
   if (hipMalloc(&m, bytes) != hipSuccess) return XYWS_ERR_NOMEM;
   if (s->lmem) {
@@ -4510,6 +4516,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     PL.lat = static_cast<uint64_t*>(s->lmem);
     PL.lgrp = PL.lat + LW_STAT + s->lmax_segs;
     PL.lbrk = PL.lat + lat_rep_off(s->lmax_segs);
+    PL.lsl = PL.lat + lat_sl_off(s->lmax_segs);
     PL.nseg = lnseg;
     const uint64_t maxg = small ? 64 : (uint64_t)s->ncu * (two ? G_LAT2::WPC : G_LAT::WPC);
     const uint32_t grid = (uint32_t)(lnseg < maxg ? lnseg : maxg);
