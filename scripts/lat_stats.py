@@ -25,6 +25,10 @@ def main():
     T = _lib.load_tools()
     buf, info = bench.build_batch(torch, T, cfg, 0, 1)
     dec = ws.frame_decoder(opts=_lib.OPT_LATTICE | xopts)
+    if os.environ.get("LAT_STATS_PREV"):  # (a call on another config first: the choice's history)
+        pb = bench.build_batch(torch, T, os.environ["LAT_STATS_PREV"], 0, 1)[0]
+        ws.frame_decoder(ctx=dec.ctx).decode(pb, cap=0, count=False, carry=False)
+        del pb
     dec.ctx.reserve(info["size"], 0)
     for _ in range(6):
         dec.decode(buf, cap=0, count=False, carry=False)
@@ -44,7 +48,7 @@ def main():
            "segments": int(out[27]), "policy": list(pol), "segments_per_workgroup": round(int(out[27]) / 512, 1)}
     for k, n in NAMES.items():
         res["us_per_segment_" + n] = round(out[k] / segs / 2100.0, 3)
-    res["us_end_check_per_workgroup"] = round(out[29] / max(1, int(sys.argv[3]) if len(sys.argv) > 3 else 256) / 2100.0, 3)
+    res["us_gate_wait_per_workgroup"] = round(out[29] / max(1, int(sys.argv[3]) if len(sys.argv) > 3 else 256) / 2100.0, 3)
     print(json.dumps(res), flush=True)
 
 

@@ -354,11 +354,15 @@ inline constexpr uint64_t lat_rep_off(uint64_t segs) {
   return (LW_STAT + segs + segs / 64 + 1 + LAT_REPW - 1) / LAT_REPW * LAT_REPW;
 }
 inline constexpr uint64_t lat_sl_off(uint64_t segs) { return lat_rep_off(segs) + LAT_NREP * LAT_REPW; }
+// The replicas only when the word itself moved (a break no earlier than one
+// already recorded changes nothing; a replica behind the word costs only
+// speculation, every decision that must be exact reads the word).
 XYWS_DEV void lat_raise_brk(const run_params& P, uint64_t k, uint32_t lane) {
   uint64_t o = 0;
   if (lane == 0) o = __hip_atomic_fetch_max(P.lat + LW_BRK, ~k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (uniform64(o) >= ~k) return;  // (the returning atomic's wait: the compiler's)
   __hip_atomic_fetch_max(P.lbrk + LAT_REPW * lane, ~k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(o)::"memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // The claim wave's extra loads for segment s, one dword per lane, issued with
@@ -581,13 +585,18 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
     const bool gate = it == 0 && !blind;
     if (CT && tid < 64) {
       // the segment's own result, published while the data waves store
-      if (brk != NONE32) lat_raise_brk(P, ka + brk, lane);  // (completed before the result is published)
+      // (completed before the result is published; nothing to raise when an
+      // earlier failing point is known already)
+      const uint64_t gk = uniform64(L.gk);
+      if (brk != NONE32 && !(gk && ~gk <= ka + brk)) lat_raise_brk(P, ka + brk, lane);
       if (tid == 0) {
         st_store(P.lat + LW_STAT + cur, (E << 2) | (brk != NONE32 ? LS_BRK : LS_AGG));
         __hip_atomic_fetch_add(P.lgrp + cur / LAT_GRP, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (gate) {
+        const uint64_t tg = clk.on ? __builtin_amdgcn_s_memtime() : 0;
         lat_wait_decided(P, E, cur, lane);
+        if (tg && tid == 0) stat_add(P, LT_END, __builtin_amdgcn_s_memtime() - tg);  // (stats: the gate's wait)
         if (tid == 0) L.gk = st_load(P.lat + LW_BRK);
       }
       // the load for the next segment's decision (the last operation of the
@@ -850,12 +859,37 @@ __attribute__((amdgpu_waves_per_eu(G::NT * G::WPC >= 256 ? G::NT * G::WPC / 256 
   __syncthreads();
   const uint64_t kb = L.kbf;
   if (kb != NONE) {
-    for (uint32_t w = 0; w < gridDim.x; w++) {
+    // the stores to undo, from every workgroup's list at once (one thread per
+    // list) into this workgroup's own list in LDS; more than it holds: one
+    // list at a time (rare twice over)
+    if (tid == 0) L.nsl = 0;
+    __syncthreads();
+    for (uint32_t w = tid; w < gridDim.x; w += G::NT) {
       const uint64_t* q = P.lsl + (uint64_t)w * LAT_LSW;
       const uint32_t n = (uint32_t)st_load(q);
       for (uint32_t i = 0; i < n; i++) {
         const uint64_t kst = st_load(q + 2 + 2 * i);
-        if (kb < kst) lat_undo<G>(P, L, tid, st_load(q + 1 + 2 * i), kst, kb);
+        if (kb < kst) {
+          const uint32_t j = atomicAdd(&L.nsl, 1u);
+          if (j < LAT_SLIST) {
+            L.sl_seg[j] = st_load(q + 1 + 2 * i);
+            L.sl_k[j] = kst;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t nu = L.nsl;
+    if (nu <= LAT_SLIST) {
+      for (uint32_t j = 0; j < nu; j++) lat_undo<G>(P, L, tid, L.sl_seg[j], L.sl_k[j], kb);
+    } else {
+      for (uint32_t w = 0; w < gridDim.x; w++) {
+        const uint64_t* q = P.lsl + (uint64_t)w * LAT_LSW;
+        const uint32_t n = (uint32_t)st_load(q);
+        for (uint32_t i = 0; i < n; i++) {
+          const uint64_t kst = st_load(q + 2 + 2 * i);
+          if (kb < kst) lat_undo<G>(P, L, tid, st_load(q + 1 + 2 * i), kst, kb);
+        }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

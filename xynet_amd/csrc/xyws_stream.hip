@@ -4526,6 +4526,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     if (rc) return rc;
     P.lat = PL.lat;
     P.opts |= XYWS_OPT_REDIRECT;
+    if (opts & XYWS_OPT_LATX_ONLY) return XYWS_OK;  // (timing experiment: the lattice kernel alone)
   }
   return small ? launch_runs<G_SMALL>(P, stream)
                : wg512 ? launch_runs<G_PROD2>(P, stream) : launch_runs<G_PROD>(P, stream);
