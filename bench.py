@@ -365,7 +365,7 @@ def source_hash():
 
 
 def pmc_traffic(config, mode):
-    """HBM bytes per k_stream_runs launch from profiles/pmc_traffic.json when
+    """HBM bytes per decoder kernel launch from profiles/pmc_traffic.json when
     that record was measured on these exact decoder sources; else None."""
     pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(pmc_file):

@@ -17,20 +17,26 @@ import sys
 
 def per_launch(d, counter, kernel=None):
     """Average counter value per launch of `kernel` (a name substring); by
-    default the decoder kernel (k_stream_runs / k_stream_sweep) of the last
-    dispatch, i.e. the one the timed steps ran (the decoder choice serves the
-    first calls, before the first one has finished, with the run decoder)."""
-    vals, last = {}, None
+    default the decoder kernel (k_stream_lattice / k_stream_runs /
+    k_stream_sweep) of the last dispatches, i.e. the one the timed steps ran
+    (the decoder choice serves the first calls, before the first one has
+    finished, with the run decoder); after a lattice launch the run decoder
+    that follows it reads the redirect record and exits: the lattice's counts."""
+    names = ("k_stream_lattice", "k_stream_runs", "k_stream_sweep")
+    vals, last, prev = {}, None, None
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         rows = list(csv.DictReader(open(f)))
         if rows and "Dispatch_Id" in rows[0]:
             rows.sort(key=lambda r: int(r["Dispatch_Id"]))
         for r in rows:
             name = r["Kernel_Name"]
-            hit = (kernel in name) if kernel else ("k_stream_runs" in name or "k_stream_sweep" in name)
+            hit = (kernel in name) if kernel else any(n in name for n in names)
             if hit and r["Counter_Name"] == counter:
-                k = "k_stream_sweep" if "k_stream_sweep" in name else ("k_stream_runs" if "k_stream_runs" in name
-                                                                        else kernel)
+                k = kernel or next(n for n in names if n in name)
+                redirect = prev == "k_stream_lattice" and k == "k_stream_runs"  # (the lattice's hand-over check)
+                prev = k
+                if redirect:
+                    continue
                 vals.setdefault(k, []).append(float(r["Counter_Value"]))
                 last = k
     if not vals:
@@ -44,7 +50,7 @@ def source_hash():
     import hashlib
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     h = hashlib.sha256()
-    for f in ("xyws_stream.hip", "xyws_device.h", "xyws_stream.h", "xyws.hip"):
+    for f in ("xyws_stream.hip", "xyws_device.h", "xyws_stream.h", "xyws.hip", "xyws_lattice.h"):
         with open(os.path.join(root, "xynet_amd", "csrc", f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]

@@ -1,10 +1,11 @@
 #!/bin/bash
 # The profile set behind DESIGN.md §7, on the committed sources, on the GPU box:
-#   TAG=r04a STEPS="tests bench prof pmc ops compat host echo small" scripts/profile_set.sh
+#   TAG=r04a STEPS="tests smoke bench prof pmc ops compat host echo small" scripts/profile_set.sh
 # Every step runs under its own time limit and the set stops at the first
 # failing step (a GPU fault, a timeout, a failed test); outputs go to
 # gpurun_out/${TAG}_*; copy the summaries worth keeping into profiles/.
-#   tests   pytest -m gpu + smoke()
+#   tests   pytest -m gpu
+#   smoke   __graft_entry__.smoke()
 #   bench   bench.py lines for CFGS (default c3 c2 c1 c4; c3 with the CPU baseline and copy ceiling)
 #   prof    rocprofv3 --kernel-trace --stats per config + steady-state summary (trace_summary.py)
 #   pmc     FETCH_SIZE and WRITE_SIZE passes per config (separate runs; pmc_summary.py folds them)
@@ -21,10 +22,8 @@ CFGS=${CFGS:-"c3 c2 c1 c4"}
 BENCH=${BENCH_ARGS:-}
 step() { local n=$1 s=$2; shift 2; echo "== $n $(date +%T)"; timeout -k 10 $s "$@" > gpurun_out/${T}_$n.log 2>&1; local rc=$?; echo "== $n rc=$rc"; tail -1 gpurun_out/${T}_$n.log | cut -c1-240; [ $rc -eq 0 ] || exit $rc; }
 has() { case " $STEPS " in *" $1 "*) return 0;; esac; return 1; }
-if has tests; then
-  step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
-  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-fi
+has tests && step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+has smoke && step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 if has bench; then
   for c in $CFGS; do
     if [ "$c" = c3 ]; then step bench_$c 400 python bench.py --config $c $BENCH
