@@ -107,19 +107,29 @@ __global__ void __launch_bounds__(UNMASK_NT) k_unmask_range(uint8_t* __restrict_
         e[u] = __builtin_amdgcn_raw_buffer_load_b128(r, t * 16u, u * UNMASK_NT * 16u, 2);
     }
     const auto w = rsrc(cur);
+    // (a tile away from both ends stores every chunk whole: a uniform branch)
+    const uint64_t tc = c0 + cur * TILE;  // the tile's first chunk
+    if (tc << 4 >= lo && (tc + TILE) << 4 <= hi) {
 #pragma unroll
-    for (uint32_t u = 0; u < UNMASK_U; u++) {
-      const uint64_t c = c0 + cur * TILE + u * UNMASK_NT + t;  // absolute chunk
-      const uint64_t a = c << 4;
-      const bool whole = a >= lo && a + 16 <= hi;
-      __builtin_amdgcn_raw_buffer_store_b128(d[u], w, whole ? t * 16u : 0x80000000u, u * UNMASK_NT * 16u, 2);
-      // (the store's data registers stay live past the next store)
-      asm volatile("" ::"v"(d[u].x), "v"(d[u].y), "v"(d[u].z), "v"(d[u].w));
-      if (!whole && c < c1) {  // an edge chunk: its in-range bytes
-        for (uint32_t b = 0; b < 16; b++) {
-          const uint64_t q = a + b;
-          const uint32_t wd = b < 4 ? d[u].x : b < 8 ? d[u].y : b < 12 ? d[u].z : d[u].w;
-          if (q >= lo && q < hi) base[q] = (uint8_t)(wd >> (8u * (b & 3u)));
+      for (uint32_t u = 0; u < UNMASK_U; u++) {
+        __builtin_amdgcn_raw_buffer_store_b128(d[u], w, t * 16u, u * UNMASK_NT * 16u, 2);
+        // (the store's data registers stay live past the next store)
+        asm volatile("" ::"v"(d[u].x), "v"(d[u].y), "v"(d[u].z), "v"(d[u].w));
+      }
+    } else {
+#pragma unroll
+      for (uint32_t u = 0; u < UNMASK_U; u++) {
+        const uint64_t c = tc + u * UNMASK_NT + t;  // absolute chunk
+        const uint64_t a = c << 4;
+        const bool whole = a >= lo && a + 16 <= hi;
+        __builtin_amdgcn_raw_buffer_store_b128(d[u], w, whole ? t * 16u : 0x80000000u, u * UNMASK_NT * 16u, 2);
+        asm volatile("" ::"v"(d[u].x), "v"(d[u].y), "v"(d[u].z), "v"(d[u].w));
+        if (!whole && c < c1) {  // an edge chunk: its in-range bytes
+          for (uint32_t b = 0; b < 16; b++) {
+            const uint64_t q = a + b;
+            const uint32_t wd = b < 4 ? d[u].x : b < 8 ? d[u].y : b < 12 ? d[u].z : d[u].w;
+            if (q >= lo && q < hi) base[q] = (uint8_t)(wd >> (8u * (b & 3u)));
+          }
         }
       }
     }
