@@ -22,15 +22,18 @@ OPT_STEAL = 0x400000        # work stealing (off by default)
 OPT_TEST_STEAL = 0x800000   # every fourth run starts late; pieces of 1 segment and up are taken
 OPT_UNMASKED_HINT = 0x2     # include/xyws.h: speculate on server->client framing (wrong for these streams)
 OPT_WG512 = 0x40000         # two 512-thread workgroups per CU, 64 KiB segments
+OPT_WG256 = 0x8             # four 256-thread workgroups per CU, 16 KiB segments
+OPT_NO_LATDEC = 0x800       # the run decoder itself (equal frames would take the lattice decoder)
 MODES = {"fused": {}, "serial": {"serial": True}, "runs1k": {"small_segments": True},
-         "wg512": {"opts": OPT_WG512}, "wrong_hint": {"opts": OPT_UNMASKED_HINT},
+         "wg512": {"opts": OPT_WG512 | OPT_NO_LATDEC}, "wg256": {"opts": OPT_WG256 | OPT_NO_LATDEC},
+         "wrong_hint": {"opts": OPT_UNMASKED_HINT | OPT_NO_LATDEC},
          "runs1k_wrong_hint": {"small_segments": True, "opts": OPT_UNMASKED_HINT},
-         "giveup": {"opts": OPT_TEST_GIVEUP},
+         "giveup": {"opts": OPT_TEST_GIVEUP | OPT_NO_LATDEC},
          "runs1k_giveup": {"small_segments": True, "opts": OPT_TEST_GIVEUP},
-         "steal_prod": {"opts": OPT_STEAL},
-         "steal": {"opts": OPT_TEST_STEAL},
+         "steal_prod": {"opts": OPT_STEAL | OPT_NO_LATDEC},
+         "steal": {"opts": OPT_TEST_STEAL | OPT_NO_LATDEC},
          "runs1k_steal": {"small_segments": True, "opts": OPT_TEST_STEAL},
-         "steal_giveup": {"opts": OPT_TEST_STEAL | OPT_TEST_GIVEUP},
+         "steal_giveup": {"opts": OPT_TEST_STEAL | OPT_TEST_GIVEUP | OPT_NO_LATDEC},
          "runs1k_steal_giveup": {"small_segments": True, "opts": OPT_TEST_STEAL | OPT_TEST_GIVEUP}}
 
 
@@ -400,6 +403,7 @@ CONFIG_CASES = ([(n, "fused") for n in [
     "t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m", "c1_text_4k", "c2_bin_256", "c3_bin_64k",
     "c4_mixed", "c5_shard0", "c5_shard1", "c5_shard4", "c5_shard5", "c5_shard6", "c5_shard7"]] +
     [(n, "wg512") for n in ["t_mixed_8m", "c1_text_4k", "c2_bin_256", "c3_bin_64k", "c4_mixed"]] +
+    [(n, "wg256") for n in ["t_mixed_8m", "c1_text_4k", "c2_bin_256", "c4_mixed"]] +
     [(n, "wrong_hint") for n in ["t_bin_256_x4096", "c4_mixed"]] +
     [(n, "runs1k") for n in ["t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m"]] +
     [(n, "giveup") for n in ["t_mixed_8m", "c1_text_4k", "c2_bin_256", "c4_mixed", "c5_shard3"]] +

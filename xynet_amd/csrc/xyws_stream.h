@@ -72,6 +72,7 @@ int stream_scratch_unmask_counter(stream_scratch* s, bool capturing, uint32_t** 
 #define XYWS_OPT_NO_LATDEC 0x800u    // never the lattice decoder
 #define XYWS_OPT_TEST_LATSPEC 0x10u  // tests (lattice decoder): every store speculative (no first-segment gate, no
                                      // failing-point filter): a broken lattice is undone by the end-of-work check
+#define XYWS_OPT_WG256 0x8u  // the run decoder in four 256-thread workgroups per CU on 16 KiB segments
 #define XYWS_OPT_LATX_ONLY 0x80u  // timing experiment only (wrong bytes after a redirect): no run decoder after the lattice
 #define XYWS_OPT_LATX_2WG 0x20u  // experiment (lattice decoder): the two-workgroups-per-CU geometry (G_LAT2)
 #define XYWS_OPT_LATX_NOWORK 0x40u  // timing experiment only (wrong bytes): the lattice decoder's data waves skip

@@ -122,6 +122,7 @@ struct geom {
 using G_PROD = geom<1024, 8, 4>;  // 128 KiB segments, 16 waves, one workgroup per CU (default)
 using G_PROD2 = geom<512, 8, 4>;  // 64 KiB segments, 8 waves, two workgroups per CU (XYWS_OPT_WG512)
 using G_SMALL = geom<64, 1, 1>;   // 1 KiB segments, one wave (XYWS_OPT_SMALL_SEG)
+using G_MID = geom<256, 4, 4>;    // 16 KiB segments, 4 waves, four workgroups per CU (mid_preferred)
 using G_SWEEP = geom<1024, 8, 4, true>;  // the sweep decoder: 128 KiB segments
 using G_SWEEP_SMALL = geom<64, 1, 1, true>;  // the sweep decoder on 1 KiB segments (tests)
 
@@ -4345,6 +4346,16 @@ static bool sweep_preferred(const stream_scratch* s, uint64_t len) {
 // segment, and a run's latency is the call's): echo-sized batches of 0-1000 B
 // frames 115-135 -> 72-79 us per call (profiles/r03z_echo_geometry.txt).
 constexpr uint64_t WG512_MAX_FRAME = 2048;
+// Echo-sized batches (under 32 KiB per CU) of small frames of mixed sizes:
+// four 256-thread workgroups per CU on 16 KiB segments, four times the runs
+// of the 512-thread geometry (a run's latency is the call's: 4 MiB of 0-1000 B
+// frames with descriptors 80.6 -> 65.7 us, 1 MiB 81.9 -> 57.4; 8 KiB segments
+// 78.9 / 53.6; at 16 MiB the 512-thread geometry stays faster, 94 vs 125).
+static bool mid_preferred(const stream_scratch* s, uint64_t len) {
+  if (!s->pol_h) return false;
+  const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
+  return fsmax && fsmax < WG512_MAX_FRAME && fsmin != fsmax && len <= (uint64_t)s->ncu * 32768;
+}
 constexpr uint64_t DENSE0_MAX_FRAME = 2048;
 static bool wg512_preferred(const stream_scratch* s, uint64_t len) {
   if (!s->pol_h) return false;
@@ -4436,14 +4447,16 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     const uint32_t grid = (uint32_t)(nseg < maxg ? nseg : maxg);
     return small ? launch_sweep<G_SWEEP_SMALL>(P, grid, stream) : launch_sweep<G_SWEEP>(P, grid, stream);
   }
-  const bool wg512 = !small && !(opts & XYWS_OPT_WG1024) && ((opts & XYWS_OPT_WG512) || wg512_preferred(s, hi - lo));
-  const uint64_t seg = small ? G_SMALL::SEG : wg512 ? G_PROD2::SEG : G_PROD::SEG;
+  const bool mid = !small && !(opts & (XYWS_OPT_WG512 | XYWS_OPT_WG1024)) &&
+                   ((opts & XYWS_OPT_WG256) || mid_preferred(s, hi - lo));
+  const bool wg512 = !small && !mid && !(opts & XYWS_OPT_WG1024) && ((opts & XYWS_OPT_WG512) || wg512_preferred(s, hi - lo));
+  const uint64_t seg = small ? G_SMALL::SEG : mid ? G_MID::SEG : wg512 ? G_PROD2::SEG : G_PROD::SEG;
   // Runs get equal byte ranges (multiples of 16, one segment at least): every
   // workgroup streams the same number of bytes, and a run whose chain crosses
   // into the next range loads only the bytes below the successor's W there.
   const uint64_t nseg = (hi + seg - 1) / seg;
   uint64_t nruns, rbytes;
-  const uint64_t r = small ? nseg : (uint64_t)s->ncu * (wg512 ? 2u : 1u);
+  const uint64_t r = small ? nseg : (uint64_t)s->ncu * (mid ? 4u : wg512 ? 2u : 1u);
   const uint64_t maxr = r < MAX_RUNS ? r : MAX_RUNS;
   if (nseg <= maxr) {
     rbytes = seg;
@@ -4529,5 +4542,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     if (opts & XYWS_OPT_LATX_ONLY) return XYWS_OK;  // (timing experiment: the lattice kernel alone)
   }
   return small ? launch_runs<G_SMALL>(P, stream)
-               : wg512 ? launch_runs<G_PROD2>(P, stream) : launch_runs<G_PROD>(P, stream);
+         : mid   ? launch_runs<G_MID>(P, stream)
+         : wg512 ? launch_runs<G_PROD2>(P, stream)
+                 : launch_runs<G_PROD>(P, stream);
 }
