@@ -203,6 +203,28 @@ int xyws_decode_stream(xyws_ctx* ctx, void* dev_buf, uint64_t len,
                        xyws_frame* dev_frames, uint64_t cap, uint64_t* dev_nframes,
                        uint32_t opts, void* stream);
 
+/* One piece of a buffer sequence: device memory. */
+typedef struct xyws_iov {
+  void*    base;
+  uint64_t len;
+} xyws_iov;
+#define XYWS_IOV_MAX 64u
+/* xyws_decode_stream over a buffer sequence — what one recv into a
+ * multi-buffer `buffer_sequence` fills (include/xynet/buffer.h:94-110,
+ * socket/impl/recv_all.h:99-121): the `niov` pieces (a HOST array of device
+ * pieces, at most XYWS_IOV_MAX, any lengths and alignments, 0-length pieces
+ * allowed) are ONE stream, decoded as if concatenated; every piece is
+ * unmasked in place. Descriptor offsets count bytes across the pieces in
+ * order (piece k starts at the sum of the earlier pieces' lengths). Three
+ * launches whatever niov (gather into the stream's staging buffer, one
+ * decode, scatter back); the staging buffer grows to the largest total seen
+ * (XYWS_ERR_CAPACITY under capture before it has). XYWS_OPT_SERIAL_SCAN is
+ * refused (XYWS_ERR_INVALID). */
+int xyws_decode_stream_iov(xyws_ctx* ctx, const xyws_iov* iov, uint32_t niov,
+                           const xyws_carry* dev_carry_in, xyws_carry* dev_carry_out,
+                           xyws_frame* dev_frames, uint64_t cap, uint64_t* dev_nframes,
+                           uint32_t opts, void* stream);
+
 
 /* ==== ABI 2: the rest of the frame interface ============================ */
 

@@ -147,6 +147,8 @@ def load():
     L.xyws_debug_records.argtypes = [vp, vp, C.POINTER(C.c_uint64), u64]
     L.xyws_decode_stream.restype = i32
     L.xyws_decode_stream.argtypes = [vp, vp, u64, vp, vp, vp, u64, vp, u32, vp]
+    L.xyws_decode_stream_iov.restype = i32
+    L.xyws_decode_stream_iov.argtypes = [vp, vp, u32, vp, vp, vp, u64, vp, u32, vp]
     # ABI 2
     L.xyws_parser_create.restype = i32
     L.xyws_parser_create.argtypes = [vp, C.POINTER(vp)]

@@ -392,6 +392,8 @@ int xyws_ctx_create(int device, xyws_ctx** out) {
     sl.tab_mem = nullptr;
     sl.aux_mem = nullptr;
     sl.aux_cap = 0;
+    sl.iov_mem = nullptr;
+    sl.iov_cap = 0;
     sl.tab_cap = 0;
     stream_scratch_init(&sl.ss, device);
   }
@@ -416,6 +418,7 @@ int xyws_ctx_destroy(xyws_ctx* ctx) {
     for (auto& sl : ctx->slot) {
       if (sl.tab_mem) (void)hipFree(sl.tab_mem);
       if (sl.aux_mem) (void)hipFree(sl.aux_mem);
+      if (sl.iov_mem) (void)hipFree(sl.iov_mem);
       stream_scratch_free(&sl.ss);
     }
     if (ctx->err) (void)hipFree(ctx->err);
@@ -654,6 +657,73 @@ int xyws_decode_stream(xyws_ctx* ctx, void* dev_buf, uint64_t len, const xyws_ca
   }
   return stream_decode_fused(&sl->ss, base, lo, hi, dev_carry_in, dev_carry_out, dev_frames, cap,
                              dev_nframes, opts, s);
+}
+
+// ---------------------------------------------------------------------------
+// xyws_decode_stream_iov: a recv's buffer sequence (buffer.h:94-110, filled by
+// recv_all.h:99-121) decoded as one stream — the pieces gathered into the
+// slot's staging buffer by one launch, one fused decode there, the bytes
+// scattered back by one launch: three launches whatever the piece count (one
+// decode per piece would cost a decode's fixed latency each). The piece
+// table travels in the kernel arguments.
+struct iov_args {
+  uint8_t* base[XYWS_IOV_MAX];
+  uint64_t len[XYWS_IOV_MAX];
+  uint64_t off[XYWS_IOV_MAX];  // the piece's start in the staging buffer
+};
+// One piece per blockIdx.y; lane j of the grid copies bytes j, j + stride, ...
+// (a wave moves 64 consecutive bytes per instruction: one line either side,
+// whatever the two alignments). to_stage: pieces -> stage, else back.
+__global__ void __launch_bounds__(256) k_iov_copy(iov_args A, uint8_t* __restrict__ stage, int to_stage) {
+  const uint32_t k = blockIdx.y;
+  uint8_t* p = A.base[k];
+  uint8_t* q = stage + A.off[k];
+  const uint64_t n = A.len[k];
+  for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += (uint64_t)gridDim.x * 256) {
+    if (to_stage) q[j] = __builtin_nontemporal_load(p + j);
+    else __builtin_nontemporal_store(q[j], p + j);
+  }
+}
+
+int xyws_decode_stream_iov(xyws_ctx* ctx, const xyws_iov* iov, uint32_t niov, const xyws_carry* dev_carry_in,
+                           xyws_carry* dev_carry_out, xyws_frame* dev_frames, uint64_t cap,
+                           uint64_t* dev_nframes, uint32_t opts, void* stream) {
+  if (!ctx || (!iov && niov) || niov > XYWS_IOV_MAX) return XYWS_ERR_INVALID;
+  if ((opts & XYWS_OPT_SERIAL_SCAN) || !XYWS_HAVE_FUSED) return XYWS_ERR_INVALID;  // (the fused path only)
+  iov_args A;
+  uint64_t total = 0, longest = 0;
+  for (uint32_t k = 0; k < niov; k++) {
+    if (!iov[k].base && iov[k].len) return XYWS_ERR_INVALID;
+    A.base[k] = static_cast<uint8_t*>(iov[k].base);
+    A.len[k] = iov[k].len;
+    A.off[k] = total;
+    total += iov[k].len;
+    if (iov[k].len > longest) longest = iov[k].len;
+  }
+  if (total >= (1ull << 46) - 64) return XYWS_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  device_guard g(ctx->device);
+  if (!g.ok) return XYWS_ERR_HIP;
+  hipStream_t s = (hipStream_t)stream;
+  const bool capt = capturing(s);
+  scratch_slot* sl = nullptr;
+  int rc = acquire_slot(ctx, s, capt, &sl);
+  if (rc) return rc;
+  if ((rc = ensure_iov(sl, total + 16, capt))) return rc;
+  uint8_t* stage = static_cast<uint8_t*>(sl->iov_mem);
+  const dim3 grid((uint32_t)grid_for(longest, 256, 1024), niov ? niov : 1);
+  if (niov && total) {
+    hipLaunchKernelGGL(k_iov_copy, grid, dim3(256), 0, s, A, stage, 1);
+    if ((rc = hip_err(hipGetLastError()))) return rc;
+  }
+  if ((rc = stream_decode_fused(&sl->ss, stage, 0, total, dev_carry_in, dev_carry_out, dev_frames, cap,
+                                dev_nframes, opts, s)))
+    return rc;
+  if (niov && total && !(opts & XYWS_OPT_PARSE_ONLY)) {
+    hipLaunchKernelGGL(k_iov_copy, grid, dim3(256), 0, s, A, stage, 0);
+    if ((rc = hip_err(hipGetLastError()))) return rc;
+  }
+  return XYWS_OK;
 }
 
 // ---------------------------------------------------------------------------

@@ -38,6 +38,9 @@ struct scratch_slot {
   // frame-list kernels' scratch (xyws_frames.hip): block sums, message tables
   void* aux_mem;
   uint64_t aux_cap;
+  // xyws_decode_stream_iov: the pieces of one buffer sequence, gathered
+  void* iov_mem;
+  uint64_t iov_cap;
 };
 
 struct xyws_ctx {
@@ -165,6 +168,22 @@ inline int ensure_aux(scratch_slot* sl, uint64_t bytes, bool capture) {
   }
   sl->aux_mem = mem;
   sl->aux_cap = cap;
+  return XYWS_OK;
+}
+
+// The iov staging buffer of at least `bytes` (ctx->mu held).
+inline int ensure_iov(scratch_slot* sl, uint64_t bytes, bool capture) {
+  if (bytes <= sl->iov_cap && sl->iov_mem) return XYWS_OK;
+  if (capture) return XYWS_ERR_CAPACITY;
+  uint64_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
+  void* mem = nullptr;
+  if (hipMalloc(&mem, cap) != hipSuccess) return XYWS_ERR_NOMEM;
+  if (sl->iov_mem) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(sl->iov_mem);
+  }
+  sl->iov_mem = mem;
+  sl->iov_cap = cap;
   return XYWS_OK;
 }
 

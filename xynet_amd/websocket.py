@@ -257,6 +257,27 @@ class frame_decoder:
             "xyws_decode_stream")
         return DecodeResult(frames_t, n_t, cap)
 
+    def decode_iov(self, bufs, cap=0, count=True, carry=True):
+        """Decode a buffer sequence (device uint8 tensors, one recv's pieces)
+        as ONE stream, every piece in place (xyws_decode_stream_iov: three
+        launches whatever the piece count). Descriptor offsets count bytes
+        across the pieces in order."""
+        import torch
+        ts = [_dev_u8(b) for b in bufs]
+        arr = (C.c_uint64 * (2 * max(len(ts), 1)))()
+        for k, t in enumerate(ts):
+            arr[2 * k], arr[2 * k + 1] = t.data_ptr(), t.numel()
+        frames_t = torch.empty(max(cap, 1) * 32, dtype=torch.uint8, device=self.device) if cap else None
+        n_t = torch.zeros(1, dtype=torch.int64, device=self.device) if count else None
+        cp = C.c_void_p(self.carry_t.data_ptr()) if carry else None
+        check(self.ctx.L.xyws_decode_stream_iov(
+            self.ctx.h, C.cast(arr, C.c_void_p), len(ts), cp, cp,
+            C.c_void_p(frames_t.data_ptr()) if frames_t is not None else None, cap,
+            C.c_void_p(n_t.data_ptr()) if n_t is not None else None, self.opts,
+            _stream(ts[0]) if ts else C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
+            "xyws_decode_stream_iov")
+        return DecodeResult(frames_t, n_t, cap)
+
 
 def decode_indexed(buf, starts, frames=True, parse_only=False):
     """Frames at known offsets (ascending): parse + unmask in place."""
