@@ -299,37 +299,43 @@ __global__ void __launch_bounds__(FT) k_tile_map(gparams G, uint64_t* map, uint6
   for (; t < t1 && t < ntiles; t++) map[t] = i;
 }
 
-// Bytes [e, e + 16) of the 16-byte little-endian vector h placed at offset 0
-// of an otherwise zero byte line (e in [-15, 15]; bytes outside h read 0).
-XYWS_DEV u32x4 window16(const uint32_t h[4], int32_t e) {
-  const uint32_t v[12] = {0u, 0u, 0u, 0u, h[0], h[1], h[2], h[3], 0u, 0u, 0u, 0u};
-  const uint32_t s = (uint32_t)(16 + e), d = s >> 2, b = s & 3u;
-  uint32_t w[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    uint32_t lo = 0u, hi = 0u;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; j++)
-      if (d == j) { lo = v[j + k]; hi = v[j + k + 1]; }
-    w[k] = b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
+// A chunk-relative position clamped to [-16, 32] (only [0, 16) matters).
+XYWS_DEV int32_t rel16(int64_t x) { return x < -16 ? -16 : x > 32 ? 32 : (int32_t)x; }
+
+// Bytes [e, e + 16) of the 16-byte little-endian vector h0..h3 placed at
+// offset 0 of an otherwise zero byte line (e in [-15, 15]): a 128-bit shift
+// on two 64-bit halves.
+XYWS_DEV u32x4 window16s(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3, int32_t e) {
+  const uint64_t lo = (uint64_t)h0 | ((uint64_t)h1 << 32), hi = (uint64_t)h2 | ((uint64_t)h3 << 32);
+  const uint32_t s = 8u * (uint32_t)(e < 0 ? -e : e), s7 = s & 63u;  // s in [0, 120]
+  uint64_t rl, rh;
+  if (e >= 0) {  // (lo, hi) >> s
+    const uint64_t x = s7 ? hi << (64u - s7) : 0ull;
+    rl = s >= 64 ? hi >> s7 : (lo >> s7) | x;
+    rh = s >= 64 ? 0ull : hi >> s7;
+  } else {  // (lo, hi) << s
+    const uint64_t x = s7 ? lo >> (64u - s7) : 0ull;
+    rh = s >= 64 ? lo << s7 : (hi << s7) | x;
+    rl = s >= 64 ? 0ull : lo << s7;
   }
-  return u32x4{w[0], w[1], w[2], w[3]};
+  return u32x4{(uint32_t)rl, (uint32_t)(rl >> 32), (uint32_t)rh, (uint32_t)(rh >> 32)};
 }
 
-// Byte-select mask (per dword, 0xFF per byte) of the chunk bytes t in [lo, hi)
-// (chunk-relative, may lie outside [0, 16)).
-XYWS_DEV u32x4 span_mask(int64_t lo, int64_t hi) {
-  uint32_t m[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int64_t a = 4 * k;
-    const int64_t l = lo > a ? (lo - a < 4 ? lo - a : 4) : 0;
-    const int64_t h = hi > a ? (hi - a < 4 ? hi - a : 4) : 0;
-    const uint32_t mh = h >= 4 ? 0xFFFFFFFFu : ((1u << (8u * (uint32_t)h)) - 1u);
-    const uint32_t ml = l >= 4 ? 0xFFFFFFFFu : ((1u << (8u * (uint32_t)l)) - 1u);
-    m[k] = h > l ? (mh & ~ml) : 0u;
-  }
-  return u32x4{m[0], m[1], m[2], m[3]};
+// Byte-select mask (0xFF per byte) of the chunk bytes t in [lo, hi), lo and
+// hi chunk-relative (rel16): bytes [0, hi) and not bytes [0, lo), each as
+// two 64-bit halves.
+XYWS_DEV void low16(int32_t n, uint64_t& m0, uint64_t& m1) {
+  const uint32_t c = (uint32_t)(n < 0 ? 0 : n > 16 ? 16 : n);
+  const uint64_t a = ~(~0ull << (8u * (c & 7u)));  // bytes [0, c mod 8)
+  m0 = c >= 8 ? ~0ull : a;
+  m1 = c >= 16 ? ~0ull : c >= 8 ? a : 0ull;
+}
+XYWS_DEV u32x4 span16(int32_t lo, int32_t hi) {
+  uint64_t h0, h1, l0, l1;
+  low16(hi, h0, h1);
+  low16(lo, l0, l1);
+  const uint64_t m0 = h0 & ~l0, m1 = h1 & ~l1;
+  return u32x4{(uint32_t)m0, (uint32_t)(m0 >> 32), (uint32_t)m1, (uint32_t)(m1 >> 32)};
 }
 
 // 16 source bytes at src offset p (signed, may start before 0 or run past the
@@ -385,7 +391,20 @@ struct gstage {
   uint64_t soff[GLDS];
   uint32_t hw[GLDS][4];
   uint32_t h[GLDS], key[GLDS];
+  uint16_t cmap[GTILE / 16];  // tiles of many items: chunk -> staged item holding its first byte
 };
+
+// Tiles of more items than this map their chunks to items while staging
+// (one LDS read per chunk instead of a binary search over the items).
+constexpr uint32_t GMAP_ITEMS = 8;
+
+// The first chunk c in [0, GTILE/16] of a tile whose first output byte
+// max(base + 16c, 0) lies at or past q = d (base: q of the tile's byte 0).
+XYWS_DEV uint32_t chunk_at(int64_t d, int64_t base) {
+  if (d <= 0 || d <= base) return 0;
+  const int64_t c = (d - base + 15) >> 4;
+  return c > (int64_t)(GTILE / 16) ? GTILE / 16 : (uint32_t)c;
+}
 
 // The gather (encode replies / message payloads): output tiles of GTILE bytes,
 // each lane four 16-byte chunks. The items touching a tile (from the tile map)
@@ -420,7 +439,9 @@ __global__ void __launch_bounds__(FT) k_gather(gparams G, const uint64_t* __rest
     __syncthreads();
     const uint64_t f0 = s_f0, f1 = s_f1;
     const bool in_lds = f1 - f0 <= GLDS;
+    const bool use_map = in_lds && f1 - f0 > GMAP_ITEMS;
     if (in_lds) {
+      const int64_t base = (int64_t)t0 - (int64_t)o0;
       for (uint64_t k = threadIdx.x; k < f1 - f0; k += FT) {
         const gitem it = item_of(G, f0 + k);
         S.dst[k] = it.dst;
@@ -428,6 +449,11 @@ __global__ void __launch_bounds__(FT) k_gather(gparams G, const uint64_t* __rest
         S.hw[k][0] = it.hw[0]; S.hw[k][1] = it.hw[1]; S.hw[k][2] = it.hw[2]; S.hw[k][3] = it.hw[3];
         S.h[k] = it.h;
         S.key[k] = it.key;
+        if (use_map) {
+          // the chunks whose first byte this item holds: [dst, dst + size)
+          const uint32_t c1 = chunk_at((int64_t)(it.dst + it.h + it.len), base);
+          for (uint32_t c = chunk_at((int64_t)it.dst, base); c < c1; c++) S.cmap[c] = (uint16_t)k;
+        }
       }
       if (threadIdx.x == 0) S.dst[f1 - f0] = G.off[f1];
     }
@@ -515,7 +541,10 @@ __global__ void __launch_bounds__(FT) k_gather(gparams G, const uint64_t* __rest
       }
       const uint32_t n = (uint32_t)(f1 - f0);
       uint32_t g = 0;
-      {
+      if (use_map) {
+        g = S.cmap[c * FT + threadIdx.x];
+        if (g >= n) g = n - 1;  // (every processed chunk is mapped: a guard)
+      } else {
         uint32_t hi = n;
         while (hi - g > 1) {
           const uint32_t m = (g + hi) >> 1;
@@ -525,25 +554,30 @@ __global__ void __launch_bounds__(FT) k_gather(gparams G, const uint64_t* __rest
       const int64_t ca = (int64_t)a - (int64_t)o0;  // q of chunk byte 0 (may be < 0 in the first chunk)
       u32x4 w = {0u, 0u, 0u, 0u};
       bool oob = false;
-      for (uint32_t k = g; k < n && (int64_t)S.dst[k] < ca + 16; k++) {
-        const int64_t ds = (int64_t)S.dst[k], de = (int64_t)S.dst[k + 1];
-        const int64_t ps = ds + S.h[k];
-        if (S.h[k] && ds < ca + 16 && ps > ca) {  // header bytes
-          uint32_t hw[4] = {S.hw[k][0], S.hw[k][1], S.hw[k][2], S.hw[k][3]};
-          const u32x4 v = window16(hw, (int32_t)(ca - ds));
-          const u32x4 m = span_mask(ds - ca, ps - ca);
-          w |= v & m;
+      // (positions relative to the chunk, clamped to [-16, 32] in 32 bits:
+      // only [0, 16) matters, and the masks below are 64-bit pairs, so that
+      // the wave's instruction count per chunk stays small — with many items
+      // per tile every wave takes these branches)
+      for (uint32_t k = g; k < n; k++) {
+        const int64_t ds64 = (int64_t)S.dst[k] - ca;
+        if (ds64 >= 16) break;
+        const uint32_t hk = S.h[k];
+        const int64_t ps64 = ds64 + hk;
+        const int32_t ds = rel16(ds64), ps = rel16(ps64), de = rel16((int64_t)S.dst[k + 1] - ca);
+        if (hk && ps > 0) {  // header bytes (the item starts before the chunk's end)
+          const u32x4 v = window16s(S.hw[k][0], S.hw[k][1], S.hw[k][2], S.hw[k][3], -ds);
+          w |= v & span16(ds, ps);
         }
-        if (de > ps && ps < ca + 16 && de > ca) {  // payload bytes
-          const int64_t d = ca - ps;  // payload index of chunk byte 0
+        if (de > ps && ps < 16 && de > 0) {  // payload bytes
+          const int64_t d = -ps64;  // payload index of chunk byte 0
           const int64_t sp = (int64_t)S.soff[k] + d;
           u32x4 v = src16(G, sp);
           const uint32_t kw = rotr8(S.key[k], (uint32_t)d);
-          const u32x4 m = span_mask(ps - ca, de - ca);
+          const u32x4 m = span16(ps, de);
           // bytes past the source read as zero (and are reported)
           const int64_t past = (int64_t)G.src_len - sp;  // chunk bytes t >= past lie past src_len
           if (past < 16) {
-            const u32x4 vm = span_mask(past, 16);
+            const u32x4 vm = span16(rel16(past), 16);
             v &= ~vm;
             const u32x4 pm = vm & m;
             if (pm.x | pm.y | pm.z | pm.w) oob = true;
