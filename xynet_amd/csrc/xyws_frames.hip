@@ -123,8 +123,7 @@ XYWS_DEV uint64_t at(uint64_t n, uint64_t i) { return Rev ? n - 1 - i : i; }
 
 // pass 1: x[idx] <- the block-local scan (exclusive if Excl); part[b] <- total
 template <class Op, bool Rev, bool Excl>
-__global__ void __launch_bounds__(FT) k_scan_local(uint64_t* x, uint64_t n, uint64_t* part) {
-  __shared__ uint64_t sh[FT / 64];
+XYWS_DEV void scan_local(uint64_t* x, uint64_t n, uint64_t* part, uint64_t* sh) {
   const uint64_t i0 = (uint64_t)blockIdx.x * SB + 4ull * threadIdx.x;
   uint64_t v[4], acc = Op::id();
 #pragma unroll
@@ -142,11 +141,15 @@ __global__ void __launch_bounds__(FT) k_scan_local(uint64_t* x, uint64_t n, uint
   }
   if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
+template <class Op, bool Rev, bool Excl>
+__global__ void __launch_bounds__(FT) k_scan_local(uint64_t* x, uint64_t n, uint64_t* part) {
+  __shared__ uint64_t sh[FT / 64];
+  scan_local<Op, Rev, Excl>(x, n, part, sh);
+}
 
 // pass 2: one block scans the nb partials exclusively in place; *total <- all
 template <class Op>
-__global__ void __launch_bounds__(FT) k_scan_parts(uint64_t* part, uint64_t nb, uint64_t* total) {
-  __shared__ uint64_t sh[FT / 64];
+XYWS_DEV void scan_parts(uint64_t* part, uint64_t nb, uint64_t* total, uint64_t* sh) {
   uint64_t carry = Op::id();
   for (uint64_t c = 0; c < nb; c += FT) {
     const uint64_t i = c + threadIdx.x;
@@ -158,17 +161,68 @@ __global__ void __launch_bounds__(FT) k_scan_parts(uint64_t* part, uint64_t nb, 
   }
   if (threadIdx.x == 0 && total) *total = carry;
 }
+template <class Op>
+__global__ void __launch_bounds__(FT) k_scan_parts(uint64_t* part, uint64_t nb, uint64_t* total) {
+  __shared__ uint64_t sh[FT / 64];
+  scan_parts<Op>(part, nb, total, sh);
+}
 
 // pass 3: x[idx] <- part[block] (op) x[idx]; exclusive scans also x[n] <- total
 template <class Op, bool Rev, bool Excl>
-__global__ void __launch_bounds__(FT) k_scan_fix(uint64_t* x, uint64_t n, const uint64_t* part,
-                                                  const uint64_t* total) {
-  const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
+XYWS_DEV void scan_fix(uint64_t* x, uint64_t n, const uint64_t* part, const uint64_t* total, uint64_t i) {
   if (Excl && i == 0 && total) x[n] = *total;
   if (i >= n) return;
   const uint64_t p = part[i / SB];
   const uint64_t j = at<Op, Rev>(n, i);
   x[j] = Op::f(p, x[j]);
+}
+template <class Op, bool Rev, bool Excl>
+__global__ void __launch_bounds__(FT) k_scan_fix(uint64_t* x, uint64_t n, const uint64_t* part,
+                                                  const uint64_t* total) {
+  scan_fix<Op, Rev, Excl>(x, n, part, total, (uint64_t)blockIdx.x * FT + threadIdx.x);
+}
+
+// Three independent scans of n values in the same three kernels (the
+// reassembly's scans come in two groups of three: one launch per pass instead
+// of three). S = scan3_spec<Op, Rev, Excl>; part: 3 * nb words.
+template <class O, bool R, bool E>
+struct scan3_spec {
+  using Op = O;
+  static constexpr bool Rev = R, Excl = E;
+};
+struct scan3_args {
+  uint64_t* x[3];
+  uint64_t* total[3];
+};
+template <class S0, class S1, class S2>
+__global__ void __launch_bounds__(FT) k_scan3_local(scan3_args A, uint64_t n, uint64_t* part, uint64_t nb) {
+  __shared__ uint64_t sh[FT / 64];
+  scan_local<typename S0::Op, S0::Rev, S0::Excl>(A.x[0], n, part, sh);
+  scan_local<typename S1::Op, S1::Rev, S1::Excl>(A.x[1], n, part + nb, sh);
+  scan_local<typename S2::Op, S2::Rev, S2::Excl>(A.x[2], n, part + 2 * nb, sh);
+}
+template <class S0, class S1, class S2>
+__global__ void __launch_bounds__(FT) k_scan3_parts(scan3_args A, uint64_t* part, uint64_t nb) {
+  __shared__ uint64_t sh[FT / 64];
+  scan_parts<typename S0::Op>(part, nb, A.total[0], sh);
+  scan_parts<typename S1::Op>(part + nb, nb, A.total[1], sh);
+  scan_parts<typename S2::Op>(part + 2 * nb, nb, A.total[2], sh);
+}
+template <class S0, class S1, class S2>
+__global__ void __launch_bounds__(FT) k_scan3_fix(scan3_args A, uint64_t n, const uint64_t* part, uint64_t nb) {
+  const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
+  scan_fix<typename S0::Op, S0::Rev, S0::Excl>(A.x[0], n, part, A.total[0], i);
+  scan_fix<typename S1::Op, S1::Rev, S1::Excl>(A.x[1], n, part + nb, A.total[1], i);
+  scan_fix<typename S2::Op, S2::Rev, S2::Excl>(A.x[2], n, part + 2 * nb, A.total[2], i);
+}
+template <class S0, class S1, class S2>
+int scan3(const scan3_args& A, uint64_t n, uint64_t* part, hipStream_t s) {
+  const uint64_t nb = (n + SB - 1) / SB;
+  if (nb) hipLaunchKernelGGL((k_scan3_local<S0, S1, S2>), dim3(nb), dim3(FT), 0, s, A, n, part, nb);
+  hipLaunchKernelGGL((k_scan3_parts<S0, S1, S2>), dim3(1), dim3(FT), 0, s, A, part, nb);
+  hipLaunchKernelGGL((k_scan3_fix<S0, S1, S2>), dim3(nb ? (n + FT - 1) / FT : 1), dim3(FT), 0, s, A, n,
+                     (const uint64_t*)part, nb);
+  return hip_err(hipGetLastError());
 }
 
 // Scan n values in place (device memory x, n+1 words when Excl && total),
@@ -682,7 +736,7 @@ __global__ void __launch_bounds__(FT) k_rs_sizes(const xyws_frame* frames, uint6
   const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
   if (i >= n) return;
   const uint64_t ne = n_eff(n, dev_n);
-  uint64_t s = 0, c = 0;
+  uint64_t s = 0, c = 0, o = 0;
   if (i < ne) {
     const xyws_frame f = frames[i];
     const uint32_t op = f.flags & XYWS_FLAG_OP_MASK;
@@ -692,38 +746,34 @@ __global__ void __launch_bounds__(FT) k_rs_sizes(const xyws_frame* frames, uint6
         s = f.payload_len;
         c = 1;
       } else {
-        orphan_flag[i] = 1;  // (a continuation outside a message: dropped)
+        o = 1;  // (a continuation outside a message: dropped)
       }
     }
   }
   sz[i] = s;
   cnt[i] = c;
+  orphan_flag[i] = o;
 }
 
-// message records: first_frame by rank (st[] exclusive-scanned = ranks);
 // starts[m] = the first frame of message m for EVERY message (also past
-// msg_cap: a record's length and frame count end at the next message's start)
-__global__ void __launch_bounds__(FT) k_rs_first(const xyws_frame* frames, uint64_t n, const uint64_t* dev_n,
-                                                 const uint64_t* rank, uint64_t* starts, xyws_message* msgs,
-                                                 uint64_t msg_cap) {
+// msg_cap: a record's length and frame count end at the next message's
+// start), by rank (st[] exclusive-scanned: frame i starts a message when the
+// rank steps after it)
+__global__ void __launch_bounds__(FT) k_rs_first(uint64_t n, const uint64_t* dev_n, const uint64_t* rank,
+                                                 uint64_t* starts) {
   const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
   const uint64_t ne = n_eff(n, dev_n);
   if (i >= ne) return;
-  const uint32_t op = frames[i].flags & XYWS_FLAG_OP_MASK;
-  if (op != XYWS_FLAG_OP_TEXT && op != XYWS_FLAG_OP_BINARY) return;
-  const uint64_t m = rank[i];
-  starts[m] = i;
-  if (m < msg_cap) {
-    msgs[m].first_frame = i;
-    msgs[m].opcode = (uint8_t)op;
-  }
+  const uint64_t r = rank[i];
+  if (rank[i + 1] != r) starts[r] = i;
 }
 
-// the rest of each record from the offsets of its start and the next start
-// (starts[]: every message's first frame, k_rs_first); continuations after
-// the last message's FIN with no message after them set bit 0x200 of the
-// device error word
-__global__ void __launch_bounds__(FT) k_rs_msgs(const uint64_t* dev_n, uint64_t n, const uint64_t* nmsg_p,
+// each record from the offsets of its start and the next start (starts[]:
+// every message's first frame, k_rs_first); continuations after the last
+// message's FIN with no message after them set bit 0x200 of the device error
+// word
+__global__ void __launch_bounds__(FT) k_rs_msgs(const xyws_frame* frames, const uint64_t* dev_n, uint64_t n,
+                                                const uint64_t* nmsg_p,
                                                 const uint64_t* off, const uint64_t* cntoff, const uint64_t* b,
                                                 const uint64_t* starts, const uint64_t* orph_rank,
                                                 uint64_t out_cap, xyws_message* msgs, uint64_t msg_cap,
@@ -738,9 +788,7 @@ __global__ void __launch_bounds__(FT) k_rs_msgs(const uint64_t* dev_n, uint64_t 
   if (m >= nm || m >= msg_cap) return;
   const uint64_t s = starts[m];
   const uint64_t ns = m + 1 < nm ? starts[m + 1] : ne;
-  msgs[m].out_off = off[s];
-  msgs[m].length = off[ns] - off[s];
-  msgs[m].nframes = cntoff[ns] - cntoff[s];
+  const uint64_t op = frames[s].flags & XYWS_FLAG_OP_MASK;
   uint32_t st = 0;
   if (b[s] < ns) st |= XYWS_MSG_COMPLETE;
   else if (m + 1 < nm) st |= XYWS_MSG_INTERRUPTED;
@@ -750,8 +798,15 @@ __global__ void __launch_bounds__(FT) k_rs_msgs(const uint64_t* dev_n, uint64_t 
   // before the previous start
   const uint64_t ps = m ? starts[m - 1] : 0;
   if (orph_rank[s] - (m ? orph_rank[ps] : 0) > 0) st |= XYWS_MSG_ORPHANS;
-  msgs[m].status = st;
-  msgs[m].reserved[0] = msgs[m].reserved[1] = msgs[m].reserved[2] = 0;
+  // the whole 40-byte record in five 8-byte stores (status, opcode and the
+  // reserved bytes as one little-endian word)
+  static_assert(sizeof(xyws_message) == 40 && offsetof(xyws_message, status) == 32, "xyws_message layout");
+  uint64_t* r = reinterpret_cast<uint64_t*>(msgs + m);
+  r[0] = s;
+  r[1] = cntoff[ns] - cntoff[s];
+  r[2] = off[s];
+  r[3] = off[ns] - off[s];
+  r[4] = (uint64_t)st | (op << 32);
 }
 
 // UTF-8 (RFC 3629) over every text message's bytes in out[out_lo + ...]; one
@@ -1043,36 +1098,38 @@ int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, const 
   // each), block partials, totals
   const uint64_t w = n + 1, nb = (n + SB - 1) / SB + 1;
   const uint64_t ntiles = ((reinterpret_cast<uintptr_t>(dev_out) & 15) + out_cap + GTILE - 1) / GTILE + 1;
-  if ((rc = ensure_aux(sl, 8 * (6 * w + nb + 4 + ntiles), capt))) return rc;
+  if ((rc = ensure_aux(sl, 8 * (6 * w + 3 * nb + 4 + ntiles), capt))) return rc;
   uint64_t* A = static_cast<uint64_t*>(sl->aux_mem);
   uint64_t *a = A, *b = A + w, *st = A + 2 * w, *off = A + 3 * w, *cnt = A + 4 * w, *orph = A + 5 * w;
-  uint64_t* part = A + 6 * w;
-  uint64_t* tot = part + nb;  // tot[0]: bytes, tot[1]: messages, tot[2], tot[3]: scratch totals
-  uint64_t* tmap = tot + 4;   // gather tile map
-  if ((rc = hip_err(hipMemsetAsync(orph, 0, 8 * w, s)))) return rc;
+  uint64_t* part = A + 6 * w;     // 3 * nb: one slice per scan of a group
+  uint64_t* tot = part + 3 * nb;  // tot[0]: bytes, tot[1]: messages, tot[2], tot[3]: scratch totals
+  uint64_t* tmap = tot + 4;       // gather tile map
   const dim3 gn((uint32_t)((n + FT - 1) / FT > 0 ? (n + FT - 1) / FT : 1));
   if (n) {
     hipLaunchKernelGGL(k_rs_marks, gn, dim3(FT), 0, s, dev_frames, n, dev_n, a, b, st);
     if ((rc = hip_err(hipGetLastError()))) return rc;
   }
-  if ((rc = scan<op_max, false, false>(a, n, part, tot + 2, s))) return rc;
-  if ((rc = scan<op_min, true, false>(b, n, part, tot + 3, s))) return rc;
+  // the last start at or before each frame, the next FIN at or after it, and
+  // the message ranks of the starts
+  if ((rc = scan3<scan3_spec<op_max, false, false>, scan3_spec<op_min, true, false>, scan3_spec<op_sum, false, true>>(
+           scan3_args{{a, b, st}, {tot + 2, tot + 3, tot + 1}}, n, part, s)))
+    return rc;
   if (n) {
     hipLaunchKernelGGL(k_rs_sizes, gn, dim3(FT), 0, s, dev_frames, n, dev_n, (const uint64_t*)a,
                        (const uint64_t*)b, off, cnt, orph);
     if ((rc = hip_err(hipGetLastError()))) return rc;
   }
-  if ((rc = scan<op_sum, false, true>(off, n, part, tot + 0, s))) return rc;
-  if ((rc = scan<op_sum, false, true>(cnt, n, part, tot + 2, s))) return rc;
-  if ((rc = scan<op_sum, false, true>(st, n, part, tot + 1, s))) return rc;
-  if ((rc = scan<op_sum, false, true>(orph, n, part, tot + 3, s))) return rc;
+  // output offsets, frame counts and orphan counts
+  if ((rc = scan3<scan3_spec<op_sum, false, true>, scan3_spec<op_sum, false, true>, scan3_spec<op_sum, false, true>>(
+           scan3_args{{off, cnt, orph}, {tot + 0, tot + 2, tot + 3}}, n, part, s)))
+    return rc;
   if (n) {
     // (a[] is free after k_rs_sizes: every message's first frame)
-    hipLaunchKernelGGL(k_rs_first, gn, dim3(FT), 0, s, dev_frames, n, dev_n, (const uint64_t*)st, a, dev_msgs,
-                       msg_cap);
+    hipLaunchKernelGGL(k_rs_first, gn, dim3(FT), 0, s, n, dev_n, (const uint64_t*)st, a);
     if ((rc = hip_err(hipGetLastError()))) return rc;
   }
-  hipLaunchKernelGGL(k_rs_msgs, gn, dim3(FT), 0, s, dev_n, n, (const uint64_t*)(tot + 1), (const uint64_t*)off,
+  hipLaunchKernelGGL(k_rs_msgs, gn, dim3(FT), 0, s, dev_frames, dev_n, n, (const uint64_t*)(tot + 1),
+                     (const uint64_t*)off,
                      (const uint64_t*)cnt, (const uint64_t*)b, (const uint64_t*)a, (const uint64_t*)orph,
                      out_cap, dev_msgs, msg_cap, dev_nmsgs, ctx->err);
   if ((rc = hip_err(hipGetLastError()))) return rc;
