@@ -893,11 +893,20 @@ __global__ void __launch_bounds__(FT) k_utf8(const uint8_t* out, uint64_t out_lo
     if (s_text) {
       // the tile's 16-byte chunks in out[] coordinates q = position - out_lo
       const uint64_t t0 = tile * UT;
-      for (uint32_t c = threadIdx.x; c < UT / 16; c += FT) {
+      // each wave walks its own UT/4 bytes row by row (a row: 64 chunks, one
+      // per lane), so a lane's next chunk usually lies in the message of its
+      // last one: once that message is known bad (random "text": in its
+      // first row) the lane skips the rest of it, loads included
+      constexpr uint32_t UROWS = UT / 16 / FT;
+      const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+      uint64_t sk0 = 1, sk1 = 0;  // q range of a message this lane needs not check
+      for (uint32_t kr = 0; kr < UROWS; kr++) {
+        const uint32_t c = (wv * UROWS + kr) * 64u + ln;
         const uint64_t a = t0 + (uint64_t)c * 16;  // out[] byte position
         if (a + 16 <= out_lo) continue;
         const uint64_t q0 = a > out_lo ? a - out_lo : 0;
         if (q0 >= total) break;
+        if (q0 >= sk0 && a + 16 - out_lo <= sk1) continue;
         // the chunk's bytes: one 16-byte load when it lies inside the written
         // range, else byte loads of the bytes that do (the rest read as 0)
         uint32_t w[4];
@@ -974,6 +983,11 @@ __global__ void __launch_bounds__(FT) k_utf8(const uint8_t* out, uint64_t out_lo
           }
         }
         if (bad) mark(m, ty);
+        // (the chunk's last message: nothing left to check in it)
+        if (bad || (ty & XYWS_MSG_UTF8_BAD) || !(ty & UTEXT)) {
+          sk0 = mo;
+          sk1 = me;
+        }
       }
     }
     __syncthreads();
