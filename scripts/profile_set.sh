@@ -9,7 +9,7 @@
 #   bench   bench.py lines for CFGS (default c3 c2 c1 c4; c3 with the CPU baseline and copy ceiling)
 #   prof    rocprofv3 --kernel-trace --stats per config + steady-state summary (trace_summary.py)
 #   pmc     FETCH_SIZE and WRITE_SIZE passes per config (separate runs; pmc_summary.py folds them)
-#   ops     the §8(f) callers on c3 and c2 (encode, classify, reassemble)
+#   ops     the §8(f) callers on c1-c4 (encode, classify, reassemble)
 #   compat  per-header latency of the compatibility path (tests/cpp/test_compat --latency)
 #   host    PCIe-inclusive host paths on c3
 #   echo    the loopback echo harness at a few receive-buffer sizes
@@ -43,7 +43,7 @@ if has pmc; then
   done
 fi
 if has ops; then
-  for c in c3 c2; do for op in encode classify reassemble; do
+  for c in c3 c2 c1 c4; do for op in encode classify reassemble; do
     step op_${op}_$c 300 python bench.py --config $c --op $op --no-cpu --no-ceiling
   done; done
 fi
