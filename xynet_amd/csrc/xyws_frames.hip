@@ -392,6 +392,19 @@ XYWS_DEV u32x4 span16(int32_t lo, int32_t hi) {
   return u32x4{(uint32_t)m0, (uint32_t)(m0 >> 32), (uint32_t)m1, (uint32_t)(m1 >> 32)};
 }
 
+// Bytes [sh, sh + 16) of the 32 bytes x | y (sh in [0, 16)): a half-select
+// (sh >= 8) and two 64-bit funnel shifts.
+XYWS_DEV u32x4 funnel16(const u32x4& x, const u32x4& y, uint32_t sh) {
+  const uint64_t x0 = (uint64_t)x.x | ((uint64_t)x.y << 32), x1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
+  const uint64_t y0 = (uint64_t)y.x | ((uint64_t)y.y << 32), y1 = (uint64_t)y.z | ((uint64_t)y.w << 32);
+  const bool h = sh >= 8;
+  const uint64_t A = h ? x1 : x0, B = h ? y0 : x1, C = h ? y1 : y0;
+  const uint32_t s = 8u * (sh & 7u);
+  const uint64_t r0 = s ? (A >> s) | (B << (64u - s)) : A;
+  const uint64_t r1 = s ? (B >> s) | (C << (64u - s)) : B;
+  return u32x4{(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32)};
+}
+
 // 16 source bytes at src offset p (signed, may start before 0 or run past the
 // end): the two aligned 16-byte lines around it, lines outside the source
 // [0, round16(src_lo + src_len)) read as zero.
@@ -404,34 +417,7 @@ XYWS_DEV u32x4 src16(const gparams& G, int64_t p) {
   const uint32_t sh = (uint32_t)(A & 15);
   if (!sh) return x;
   const u32x4 y = (a + 16 >= 0 && a + 16 < top) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(G.src + a + 16)) : z;
-  const uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-  const uint32_t d = sh >> 2, b = sh & 3u;
-  uint32_t w[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    uint32_t lo = v[k], hi = v[k + 1];
-#pragma unroll
-    for (uint32_t s = 1; s < 4; s++)
-      if (d == s) { lo = v[s + k]; hi = v[s + k + 1]; }
-    w[k] = b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
-  }
-  return u32x4{w[0], w[1], w[2], w[3]};
-}
-
-// Bytes [sh, sh + 16) of the 32 bytes x | y (sh in [0, 16)).
-XYWS_DEV u32x4 funnel16(const u32x4& x, const u32x4& y, uint32_t sh) {
-  const uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-  const uint32_t d = sh >> 2, b = sh & 3u;
-  uint32_t w[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    uint32_t lo = v[k], hi = v[k + 1];
-#pragma unroll
-    for (uint32_t s = 1; s < 4; s++)
-      if (d == s) { lo = v[s + k]; hi = v[s + k + 1]; }
-    w[k] = b ? __builtin_amdgcn_alignbyte(hi, lo, b) : lo;
-  }
-  return u32x4{w[0], w[1], w[2], w[3]};
+  return funnel16(x, y, sh);
 }
 
 XYWS_DEV u32x4 shfl_down16(const u32x4& x) {
