@@ -31,7 +31,6 @@ constexpr uint32_t FT = 256;           // threads per block, frame-list kernels
 constexpr uint32_t SB = 4 * FT;        // items per scan block (4 per lane)
 constexpr uint32_t GTILE = 16384;      // gather tile (bytes of output)
 constexpr uint32_t GLDS = 512;         // items staged per tile
-constexpr uint32_t GFAST_ITEMS = 3;    // k_gather's fast path: tiles of at most this many items
 constexpr uint64_t U64MAX = ~0ull;
 
 // ---------------------------------------------------------------- header build
@@ -405,6 +404,17 @@ XYWS_DEV u32x4 funnel16(const u32x4& x, const u32x4& y, uint32_t sh) {
   return u32x4{(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32)};
 }
 
+// Position of the n-th (from 0) set bit of m (n < popcount(m)).
+XYWS_DEV uint32_t nth_bit(uint64_t m, uint32_t n) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t w = 32; w; w >>= 1) {
+    const uint32_t c = (uint32_t)__builtin_popcountll((m >> pos) & ((1ull << w) - 1ull));
+    if (n >= c) { n -= c; pos += w; }
+  }
+  return pos;
+}
+
 // 16 source bytes at src offset p (signed, may start before 0 or run past the
 // end): the two aligned 16-byte lines around it, lines outside the source
 // [0, round16(src_lo + src_len)) read as zero.
@@ -449,15 +459,16 @@ XYWS_DEV uint32_t chunk_at(int64_t d, int64_t base) {
 // The gather (encode replies / message payloads): output tiles of GTILE bytes,
 // each lane four 16-byte chunks. The items touching a tile (from the tile map)
 // are staged in LDS once; a chunk finds its first item by a binary search in
-// LDS and is composed from at most a few items: header bytes from the staged
-// header words, payload bytes from two aligned 16-byte source loads and a
-// funnel shift, XORed with the rotated key word, each selected by its byte
+// LDS (tiles of more than GMAP_ITEMS items: the chunk map written while
+// staging). Chunks inside one item's payload (all of them for large frames)
+// take a fast path: two chunks per lane per round, and the second line a
+// misaligned chunk needs is the next lane's first (a lane shuffle), so every
+// source line is read once. The rest (item boundaries, headers) are compacted
+// per wave and composed from at most a few items: header bytes from the
+// staged header words, payload bytes from two aligned 16-byte source loads and
+// a funnel shift, XORed with the rotated key word, each selected by its byte
 // mask. One 16-byte store per chunk (byte stores only at the output's ends).
-// Chunks inside one item's payload (all of them for large frames) take a fast
-// path first: the lane's four source lines are loaded at once, and the second
-// line a misaligned chunk needs is the next lane's first (a lane shuffle), so
-// every source line is read once. Tiles with more items than fit in LDS take
-// the per-byte path.
+// Tiles with more items than fit in LDS take the per-byte path.
 __global__ void __launch_bounds__(FT) k_gather(gparams G, const uint64_t* __restrict__ map, uint64_t ntiles) {
   __shared__ gstage S;
   __shared__ uint64_t s_f0, s_f1;
@@ -500,10 +511,7 @@ __global__ void __launch_bounds__(FT) k_gather(gparams G, const uint64_t* __rest
     __syncthreads();
     constexpr uint32_t GC = GTILE / 16 / FT;
     uint32_t fastm = 0;  // chunks done by the fast path
-    // (tiles of a few large items: with many small ones most waves hold a
-    // boundary chunk in every round, and the per-chunk loop below is the whole
-    // cost: the fast path's own round trip would only add to it)
-    if (in_lds && f1 - f0 <= GFAST_ITEMS) {
+    if (in_lds) {
       const uint32_t n = (uint32_t)(f1 - f0), lane = __lane_id();
       // two chunks per round (registers: the per-chunk loop below runs in the
       // same kernel at the occupancy this path leaves)
@@ -518,10 +526,16 @@ __global__ void __launch_bounds__(FT) k_gather(gparams G, const uint64_t* __rest
         const uint64_t a = t0 + (uint64_t)(c * FT + threadIdx.x) * 16;
         const int64_t ca = (int64_t)a - (int64_t)o0;
         const uint64_t qa = a > o0 ? a - o0 : 0;
-        uint32_t g = 0, hi = n;
-        while (hi - g > 1) {
-          const uint32_t m = (g + hi) >> 1;
-          if (S.dst[m] <= qa) g = m; else hi = m;
+        uint32_t g = 0;
+        if (use_map) {
+          g = S.cmap[c * FT + threadIdx.x];
+          if (g >= n) g = n - 1;  // (a guard: every chunk in the output is mapped)
+        } else {
+          uint32_t hi = n;
+          while (hi - g > 1) {
+            const uint32_t m = (g + hi) >> 1;
+            if (S.dst[m] <= qa) g = m; else hi = m;
+          }
         }
         const int64_t ds = (int64_t)S.dst[g], de = (int64_t)S.dst[g + 1], ps = ds + S.h[g];
         const int64_t sp = (int64_t)S.soff[g] + (ca - ps);  // source payload index of chunk byte 0
@@ -556,10 +570,37 @@ __global__ void __launch_bounds__(FT) k_gather(gparams G, const uint64_t* __rest
       }
       }
     }
+    // The chunks the fast path left (item boundaries, headers, the output's
+    // ends), compacted across the wave's rounds: with small items nearly every
+    // round of every wave holds a few, and the composition below is the
+    // kernel's VALU cost — one pass over the wave's list instead of one per
+    // round. Lane i takes the i-th chunk in (round, lane) order.
+    uint32_t need = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < GC; c++) {
+      const uint64_t a = t0 + (uint64_t)(c * FT + threadIdx.x) * 16;
+      if (!(a + 16 <= o0 || a >= o1 || ((fastm >> c) & 1u))) need |= 1u << c;
+    }
+    uint64_t bm[GC];
+    uint32_t pre[GC + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < GC; r++) {
+      bm[r] = __ballot((need >> r) & 1u);
+      pre[r + 1] = pre[r] + (uint32_t)__builtin_popcountll(bm[r]);
+    }
+    const uint32_t wl = __lane_id();
 #pragma unroll 1
-    for (uint32_t c = 0; c < GTILE / 16 / FT; c++) {
-      const uint64_t a = t0 + (uint64_t)(c * FT + threadIdx.x) * 16;  // aligned out[] position
-      if (a + 16 <= o0 || a >= o1 || ((fastm >> c) & 1u)) continue;
+    for (uint32_t kb = 0; kb < pre[GC]; kb += 64) {
+      const uint32_t kk = kb + wl;
+      if (kk >= pre[GC]) break;
+      uint32_t r = 0, nn = kk;
+      uint64_t bmr = bm[0];
+#pragma unroll
+      for (uint32_t j = 1; j < GC; j++)
+        if (kk >= pre[j]) { r = j; bmr = bm[j]; nn = kk - pre[j]; }
+      const uint32_t ci = r * FT + (threadIdx.x & ~63u) + nth_bit(bmr, nn);  // the chunk, tile-relative
+      const uint64_t a = t0 + (uint64_t)ci * 16;  // aligned out[] position
       const uint64_t qa = a > o0 ? a - o0 : 0;  // first output byte of the chunk
       if (!in_lds) {
         // many tiny items: byte by byte from memory
@@ -582,7 +623,7 @@ __global__ void __launch_bounds__(FT) k_gather(gparams G, const uint64_t* __rest
       const uint32_t n = (uint32_t)(f1 - f0);
       uint32_t g = 0;
       if (use_map) {
-        g = S.cmap[c * FT + threadIdx.x];
+        g = S.cmap[ci];
         if (g >= n) g = n - 1;  // (every processed chunk is mapped: a guard)
       } else {
         uint32_t hi = n;
