@@ -160,7 +160,11 @@ int xyws_ctx_last_device_error(xyws_ctx* ctx, uint32_t* out);
 
 /* websocket_mask (websocket_frame_mask.h:6-25) on device memory: in place,
  * dev[j] ^= key[(phase + j) % 4] for j in [0, len). *phase_out (host pointer,
- * nullable) receives phase + len, the reference's return value. */
+ * nullable) receives phase + len, the reference's return value. Eager calls
+ * claim 64 KiB tiles from a counter in the stream's scratch slot (reset by
+ * the launch itself); a call captured into a graph needs no reserve and
+ * leaves no state outside its launch (static tiles), so its replays may run
+ * on any stream, concurrently with each other. */
 int xyws_unmask(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4],
                 uint64_t phase, uint64_t* phase_out, void* stream);
 

@@ -160,6 +160,50 @@ def test_irregular_streams(ws, oracle, mode):
     decode_pieces(ws, oracle, src, [0, len(src) // 3, len(src)], mode, 5)
 
 
+def _big_regular(seed, plen, nbytes, change_at=None):
+    """A regular batch of about nbytes (frames of plen payload bytes, minimal
+    16-bit form, random keys and payloads, numpy-built); frame change_at (from
+    the end when negative) has plen + 17 payload bytes."""
+    r = np.random.default_rng(seed)
+    n = nbytes // (plen + 8)
+    fr = r.integers(0, 256, size=(n, plen + 8), dtype=np.uint8)
+    fr[:, 0] = 0x82
+    fr[:, 1] = 0x80 | 126
+    fr[:, 2] = plen >> 8
+    fr[:, 3] = plen & 0xFF
+    if change_at is None:
+        return fr.reshape(-1).copy(), n
+    j = change_at % n
+    odd = r.integers(0, 256, size=plen + 17 + 8, dtype=np.uint8)
+    odd[:4] = [0x82, 0x80 | 126, (plen + 17) >> 8, (plen + 17) & 0xFF]
+    return np.concatenate([fr[:j].reshape(-1), odd, fr[j + 1:].reshape(-1)]), n
+
+
+@pytest.mark.parametrize("change_at", [None, -3])
+def test_speculation_list_overflow_hands_over(ws, oracle, change_at):
+    """The lattice decoder's speculative-store list (LAT_SLIST = 512 segments
+    per workgroup, xyws_lattice.h): past it a workgroup raises the failing
+    point to the frame before its segment and the run decoder takes the rest
+    (stores past that point undone). In 1 KiB segments (64 workgroups) a
+    regular batch above 32 MiB reaches it: 40 MiB, with and without a size
+    change near its end. Bytes, count, the whole descriptor table and the
+    carry against the oracle; the lattice did not finish the call (the run
+    decoder took the tail: policy word 4 != 3)."""
+    from test_gpu_parity import decoder_policy
+    src, n = _big_regular(0x5A17 + (change_at or 0), 4096, 40 << 20, change_at)
+    ob = src.copy()
+    oraw, ocarry, on = oracle.decode_stream_raw(ob, on_cap := n + 2)
+    t = torch.from_numpy(src.copy()).cuda()
+    dec = ws.frame_decoder(**MODES["lat1k"])
+    r = dec.decode(t, cap=on_cap)
+    assert r.nframes == on
+    assert dec.ctx.last_device_error() == 0
+    assert oracle.digest(t.cpu().numpy()) == oracle.digest(ob)
+    assert oracle.frames_digest(r.frames_t[: on * 32].cpu().numpy()) == oracle.frames_digest(oraw)
+    assert carry_list(dec.carry()) == carry_list(ocarry)
+    assert decoder_policy(dec)[4] != 3, decoder_policy(dec)
+
+
 def test_lattice_then_irregular_then_lattice(ws, oracle):
     """The decoder choice without forcing: regular batches take the lattice,
     an irregular one after them is redirected at its first size change, the

@@ -24,7 +24,9 @@ OPT_UNMASKED_HINT = 0x2     # include/xyws.h: speculate on server->client framin
 OPT_WG512 = 0x40000         # two 512-thread workgroups per CU, 64 KiB segments
 OPT_WG256 = 0x8             # four 256-thread workgroups per CU, 16 KiB segments
 OPT_NO_LATDEC = 0x800       # the run decoder itself (equal frames would take the lattice decoder)
+OPT_LATTICE = 0x400         # the lattice decoder first whatever the previous call found (the bench's decoder)
 MODES = {"fused": {}, "serial": {"serial": True}, "runs1k": {"small_segments": True},
+         "lat": {"opts": OPT_LATTICE},
          "wg512": {"opts": OPT_WG512 | OPT_NO_LATDEC}, "wg256": {"opts": OPT_WG256 | OPT_NO_LATDEC},
          "wrong_hint": {"opts": OPT_UNMASKED_HINT | OPT_NO_LATDEC},
          "runs1k_wrong_hint": {"small_segments": True, "opts": OPT_UNMASKED_HINT},
@@ -402,6 +404,8 @@ def dev_digest(buf):
 CONFIG_CASES = ([(n, "fused") for n in [
     "t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m", "c1_text_4k", "c2_bin_256", "c3_bin_64k",
     "c4_mixed", "c5_shard0", "c5_shard1", "c5_shard4", "c5_shard5", "c5_shard6", "c5_shard7"]] +
+    [(n, "lat") for n in ["c1_text_4k", "c2_bin_256", "c3_bin_64k", "c4_mixed", "c5_shard0", "c5_shard1",
+                          "c5_shard2", "c5_shard3", "c5_shard4", "c5_shard5", "c5_shard6", "c5_shard7"]] +
     [(n, "wg512") for n in ["t_mixed_8m", "c1_text_4k", "c2_bin_256", "c3_bin_64k", "c4_mixed"]] +
     [(n, "wg256") for n in ["t_mixed_8m", "c1_text_4k", "c2_bin_256", "c4_mixed"]] +
     [(n, "wrong_hint") for n in ["t_bin_256_x4096", "c4_mixed"]] +
@@ -435,6 +439,42 @@ def test_config_batches(ws, oracle, name, mode):
     assert frames_list(r.frames()[:4]) == c["first_frames"]
     assert frames_digest(oracle, r, n) == c["frames_digest"]
     assert dec.ctx.last_device_error() == 0
+    if mode == "lat":
+        # the lattice held over the whole batch (policy word 4 = 3) on the
+        # regular configs; c4 is handed to the run decoder at frame 1
+        assert (decoder_policy(dec)[4] == 3) == (name != "c4_mixed"), decoder_policy(dec)
+    del buf, r
+    torch.cuda.empty_cache()
+
+
+def decoder_policy(dec):
+    """The policy words of the last call on the current stream (xyws_debug_policy):
+    [epoch, batch bytes, smallest and largest last-frame size, decoder]."""
+    out = (C.c_uint64 * 5)()
+    stream = torch.cuda.current_stream()
+    assert dec.ctx.L.xyws_debug_policy(dec.ctx.h, C.c_void_p(stream.cuda_stream), out) == 0
+    return list(out)
+
+
+@pytest.mark.parametrize("name", ["c1_text_4k", "c2_bin_256", "c3_bin_64k", "c4_mixed", "c5_shard0", "c5_shard7"])
+def test_config_batches_bench_path(ws, name):
+    """The exact call bench.py times: the full config batch decoded in place
+    without descriptors (count on), on the decoder the choice gives a stream
+    whose previous calls were this same batch (three calls: an odd count, so
+    the payloads end unmasked). Output digest, count and carry against the
+    reference's (tests/golden/configs.json); the lattice decoder must be the
+    one that finished the regular configs."""
+    buf, c = tools_batch(name)
+    dec = ws.frame_decoder()
+    n = c["decoded_frames"]
+    for _ in range(3):
+        dec.reset()
+        r = dec.decode(buf, cap=0)
+        assert r.nframes == n
+    assert dev_digest(buf) == c["out_digest"]
+    assert carry_list(dec.carry()) == c["carry"]
+    assert dec.ctx.last_device_error() == 0
+    assert (decoder_policy(dec)[4] == 3) == (name != "c4_mixed"), decoder_policy(dec)
     del buf, r
     torch.cuda.empty_cache()
 

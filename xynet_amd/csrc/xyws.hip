@@ -47,8 +47,10 @@
 // form 5.34 TB/s; claimed 64 KiB tiles of 1024 threads x 4 chunks, two
 // workgroups per CU, 6.42 TB/s — the probe's best, with 1024 x 8 x 1 at 6.40;
 // 256-thread tiles 5.0-5.7). The two edge chunks store only their in-range
-// bytes. The last workgroup out resets the counter (graph replays start from
-// zero).
+// bytes. The last workgroup out resets the counter. ctr == nullptr (a launch
+// captured into a graph, or no scratch slot free for the stream): the same
+// loop over static tiles (workgroup b: tiles b, b + grid, ...), no state
+// outside the launch, so a replay may run on any stream, concurrently too.
 #define UNMASK_NT 1024u
 #define UNMASK_U 4u
 #define UNMASK_WPC 2u
@@ -61,10 +63,10 @@ __global__ void __launch_bounds__(UNMASK_NT) k_unmask_range(uint8_t* __restrict_
   __shared__ uint64_t s_tile;
   uint64_t ahead = ~0ull;  // thread 0: the tile claimed one tile ahead
   if (t == 0) {
-    const uint64_t a = atomicAdd(ctr, 1u);
+    const uint64_t a = ctr ? atomicAdd(ctr, 1u) : blockIdx.x;
     s_tile = a < ntiles ? a : ~0ull;
     if (a < ntiles) {
-      const uint64_t b = atomicAdd(ctr, 1u);
+      const uint64_t b = ctr ? atomicAdd(ctr, 1u) : (uint64_t)blockIdx.x + gridDim.x;
       ahead = b < ntiles ? b : ~0ull;
     }
   }
@@ -91,7 +93,7 @@ __global__ void __launch_bounds__(UNMASK_NT) k_unmask_range(uint8_t* __restrict_
     if (t == 0) {
       s_tile = ahead;
       if (ahead != ~0ull) {
-        const uint64_t b = atomicAdd(ctr, 1u);
+        const uint64_t b = ctr ? atomicAdd(ctr, 1u) : ahead + gridDim.x;
         ahead = b < ntiles ? b : ~0ull;
       }
     }
@@ -137,7 +139,7 @@ __global__ void __launch_bounds__(UNMASK_NT) k_unmask_range(uint8_t* __restrict_
     cur = nx;
   }
   __syncthreads();
-  if (t == 0) {
+  if (t == 0 && ctr) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const uint32_t n = atomicAdd(ctr + 1, 1u);
     if (n + 1 == gridDim.x) {
@@ -509,14 +511,29 @@ int xyws_debug_policy(xyws_ctx* ctx, void* stream, uint64_t* out) {
   return XYWS_ERR_INVALID;
 }
 
-// xyws_unmask with ctx->mu held: the claim counter is the stream's scratch slot's.
+// xyws_unmask with ctx->mu held: the claim counter is the stream's scratch
+// slot's when the stream has one bound or a free slot to bind (eager launches
+// only); a captured launch, or a stream finding every slot bound to others,
+// takes the static-tile form (ctr == nullptr: no state outside the launch, no
+// eviction, no device synchronization).
 static int unmask_locked(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t key[4], uint64_t phase,
                          hipStream_t s) {
-  scratch_slot* sl = nullptr;
-  int rc = acquire_slot(ctx, s, capturing(s), &sl);
-  if (rc) return rc;
   uint32_t* ctr = nullptr;
-  if ((rc = stream_scratch_unmask_counter(&sl->ss, capturing(s), &ctr))) return rc;
+  uint32_t ncu = 256;
+  if (!capturing(s)) {
+    scratch_slot* sl = nullptr;
+    bool avail = false;
+    for (auto& x : ctx->slot) avail = avail || !x.bound || x.stream == s;
+    if (avail) {
+      if (const int rc = acquire_slot(ctx, s, false, &sl)) return rc;
+      if (const int rc = stream_scratch_unmask_counter(&sl->ss, false, &ctr)) return rc;
+      ncu = (uint32_t)sl->ss.ncu;
+    } else {
+      ncu = (uint32_t)ctx->slot[0].ss.ncu;
+    }
+  } else {
+    ncu = (uint32_t)ctx->slot[0].ss.ncu;
+  }
   const uintptr_t addr = reinterpret_cast<uintptr_t>(dev);
   uint8_t* base = reinterpret_cast<uint8_t*>(addr & ~(uintptr_t)15);
   const uint64_t lo = addr & 15, hi = lo + len;
@@ -526,7 +543,7 @@ static int unmask_locked(xyws_ctx* ctx, void* dev, uint64_t len, const uint8_t k
   const uint32_t c = (uint32_t)(phase - lo) & 3u;
   const uint32_t kw = c ? ((k >> (8u * c)) | (k << (32u - 8u * c))) : k;
   const uint64_t chunks = ((hi + 15) >> 4) - (lo >> 4);
-  const uint32_t grid = grid_for(chunks, UNMASK_NT * UNMASK_U, (uint32_t)sl->ss.ncu * UNMASK_WPC);
+  const uint32_t grid = grid_for(chunks, UNMASK_NT * UNMASK_U, ncu * UNMASK_WPC);
   hipLaunchKernelGGL(k_unmask_range, dim3(grid), dim3(UNMASK_NT), 0, s, base, lo, hi, kw, ctr);
   return hip_err(hipGetLastError());
 }
@@ -692,15 +709,16 @@ int xyws_decode_stream_iov(xyws_ctx* ctx, const xyws_iov* iov, uint32_t niov, co
   if ((opts & XYWS_OPT_SERIAL_SCAN) || !XYWS_HAVE_FUSED) return XYWS_ERR_INVALID;  // (the fused path only)
   iov_args A;
   uint64_t total = 0, longest = 0;
+  constexpr uint64_t LIMIT = (1ull << 46) - 64;
   for (uint32_t k = 0; k < niov; k++) {
     if (!iov[k].base && iov[k].len) return XYWS_ERR_INVALID;
+    if (iov[k].len >= LIMIT - total) return XYWS_ERR_INVALID;  // (checked before the add: no wrap)
     A.base[k] = static_cast<uint8_t*>(iov[k].base);
     A.len[k] = iov[k].len;
     A.off[k] = total;
     total += iov[k].len;
     if (iov[k].len > longest) longest = iov[k].len;
   }
-  if (total >= (1ull << 46) - 64) return XYWS_ERR_INVALID;
   std::lock_guard<std::mutex> lk(ctx->mu);
   device_guard g(ctx->device);
   if (!g.ok) return XYWS_ERR_HIP;

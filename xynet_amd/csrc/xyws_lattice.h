@@ -9,8 +9,9 @@
 // the size of the frame there. The lattice decoder tests that hypothesis
 // everywhere at once instead of walking the list:
 //
-//  * Segments of SEG bytes are claimed in batch order from one counter, one
-//    claim ahead (the next segment's loads fly while the current one is
+//  * Segments of SEG bytes: the first round is static (workgroup b takes
+//    segments b and b + grid), then claims in batch order from one counter,
+//    one claim ahead (the next segment's loads fly while the current one is
 //    decoded), every CU streaming to the end of the batch (scripts/bw_probe6,
 //    bw_probe7).
 //  * A segment's lattice points are checked by one lane each, from the LDS
@@ -23,12 +24,20 @@
 //    bytes change).
 //  * By induction from X0 (exact: the batch start and the carry), every
 //    lattice point before the first failing one is an exact frame start. A
-//    segment publishes its own result (AGG: its points hold; BRK: one failed),
-//    then looks back over the published results of the segments before it
-//    (decoupled look-back, 64 per round; a segment that saw its prefix hold
-//    publishes INCL, which ends later look-backs) and stores only when every
-//    earlier point held: nothing is ever stored speculatively, so nothing is
-//    ever undone.
+//    segment publishes its own result (a status word, AGG: its points hold;
+//    BRK: one failed, after raising the global failing point LW_BRK) and
+//    counts in its 64-segment group. It does not wait for the segments before
+//    it: it stores every chunk below the first failing point KNOWN to it —
+//    its own, or LW_BRK as read one segment earlier (from one of 64 replicas).
+//    Only a workgroup's first segment is gated: it waits until every earlier
+//    segment has decided and reads LW_BRK fresh, so a batch that breaks near
+//    its start stores nothing wrong. Every later store is speculative: the
+//    workgroup records (segment, lattice index its stores stop at) and dumps
+//    the list to scratch at its end; the workgroup finishing the call undoes
+//    the stores past the final failing point (lat_undo: XOR is an
+//    involution, keys from the headers in memory). A workgroup whose list is
+//    full (LAT_SLIST) stops speculating: it raises the failing point to the
+//    frame before its segment and the run decoder takes the rest.
 //  * Each lane XORs its 16-byte chunks with the keys of the (at most two)
 //    frames its chunk overlaps: the frame index is arithmetic (a float
 //    reciprocal of F with a +-1 fix), no list walk.
@@ -59,8 +68,8 @@ enum {
   LW_STAT = 32     // per segment: (E << 2) | LS_*
 };
 enum { LS_AGG = 1, LS_BRK = 3 };
-constexpr uint32_t LAT_SLIST = 512;
-constexpr uint32_t LAT_NOCLAIM = 0x7FFFFFFFu;  // (no claim: the next segment after it is none)  // speculative stores a workgroup records for its end-of-work check
+constexpr uint32_t LAT_SLIST = 512;            // speculative stores a workgroup records (lat_undo's list)
+constexpr uint32_t LAT_NOCLAIM = 0x7FFFFFFFu;  // (no claim: the next segment after it is none)
 enum : uint64_t { RD_DONE = 0, RD_FULL = 1, RD_FROM = 2 };
 
 template <uint32_t NT_, uint32_t SEG_, uint32_t WPC_ = 1>
@@ -68,9 +77,9 @@ struct lgeom {
   static constexpr uint32_t NT = NT_, SEG = SEG_, WPC = WPC_;  // WPC: workgroups per CU
   static constexpr uint32_t TMAX = SEG_ / LAT_FMIN + 3;  // covering frame + lattice points
 };
-// 56 KiB segments: 8 rows of 1 KiB for each of the 7 data waves (no partial
-// last round: every wave's loads and stores are unconditional), two
-// workgroups per CU (one streams while the other checks, XORs and decides)
+// 120 KiB segments: 8 rows of 1 KiB for each of the 15 data waves (wave 0 is
+// the control wave; no partial last round: every data wave's loads and stores
+// are unconditional), one 1024-thread workgroup per CU
 using G_LAT = lgeom<1024, 15 * 8 * 1024, 1>;
 // (experiment, XYWS_OPT_LATX_2WG: 56 KiB segments for 7 data waves, two
 // 512-thread workgroups per CU)

@@ -4273,9 +4273,17 @@ int stream_scratch_unmask_counter(stream_scratch* s, bool capturing, uint32_t** 
   return XYWS_OK;
 }
 
+// The most runs any production geometry launches: four per CU (G_MID, the
+// echo-sized batches), capped at MAX_RUNS.
+static uint64_t max_prod_runs(const stream_scratch* s) {
+  const uint64_t r = (uint64_t)s->ncu * 4;
+  return r < MAX_RUNS ? r : MAX_RUNS;
+}
+
 int stream_scratch_reserve_frames(stream_scratch* s, uint64_t max_batch_bytes, uint64_t max_frames) {
-  // the production geometry: one run per CU
-  const uint64_t runs = (uint64_t)s->ncu;
+  // the descriptor regions total 8 * 2R * (2 * cap / R + 1024 + 4) bytes:
+  // largest at the most runs a production geometry launches
+  const uint64_t runs = max_prod_runs(s);
   (void)max_batch_bytes;
   const uint64_t nflat = 2 * runs;
   // (any smaller run count gives regions whose total is no larger, up to the
@@ -4284,11 +4292,18 @@ int stream_scratch_reserve_frames(stream_scratch* s, uint64_t max_batch_bytes, u
 }
 
 int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
-  // production geometry: at most one run per CU (the small-segment test mode
-  // grows scratch lazily)
-  const uint64_t nseg = (max_batch_bytes + 15 + G_PROD2::SEG - 1) / G_PROD2::SEG;
-  const uint64_t r = (uint64_t)s->ncu * 2, maxr = r < MAX_RUNS ? r : MAX_RUNS;
-  if (const int rc = scratch_grow(s, nseg < maxr ? nseg + 1 : maxr)) return rc;
+  // the production geometries (stream_decode_fused): one run per segment up
+  // to their run count (1, 2 or 4 per CU on 128, 64 or 16 KiB segments); the
+  // small-segment test mode grows scratch lazily
+  uint64_t runs = 0;
+  const uint64_t segs[3] = {G_PROD::SEG, G_PROD2::SEG, G_MID::SEG}, per_cu[3] = {1, 2, 4};
+  for (int g = 0; g < 3; g++) {
+    const uint64_t nseg = (max_batch_bytes + 15 + segs[g] - 1) / segs[g];
+    const uint64_t r = (uint64_t)s->ncu * per_cu[g], maxr = r < MAX_RUNS ? r : MAX_RUNS;
+    const uint64_t n = nseg < maxr ? nseg : maxr;
+    if (n > runs) runs = n;
+  }
+  if (const int rc = scratch_grow(s, runs)) return rc;
   // the sweep decoder's segments (production geometry)
   if (const int rc = sweep_grow(s, (max_batch_bytes + 15 + G_SWEEP::SEG - 1) / G_SWEEP::SEG, false)) return rc;
   // the lattice decoder's (production geometry)
