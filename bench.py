@@ -670,10 +670,11 @@ def main():
 
     # Settling: untimed decodes before the W warm-up steps, so that the timed
     # steps see the device's steady state. A burst of 2 GiB decodes runs
-    # through a power/clock transient: the sweep decoder's kernel time rises
-    # from ~710 to ~850 us over its first few calls and settles at ~695 us
-    # after ~18 (profiles/archive/r03j_c3_dispatch_sequence.json, r03k); the timed
-    # region is unchanged (exactly K steps), the count is in the JSON line.
+    # through a power/clock transient: round 3's (retired) sweep decoder's
+    # kernel time rose from ~710 to ~850 us over its first few calls and
+    # settled at ~695 us after ~18 (profiles/archive/r03j_c3_dispatch_sequence.json,
+    # r03k); the lattice decoder shows none. The timed region is
+    # unchanged (exactly K steps), the count is in the JSON line.
     settle = max(0, args.settle - args.warmup)
     for i in range(settle + args.warmup):
         step(i)
@@ -703,7 +704,7 @@ def main():
     if args.mode == "fused":
         pol = (C.c_uint64 * 5)()
         if dec.ctx.L.xyws_debug_policy(dec.ctx.h, C.c_void_p(stream.cuda_stream), pol) == 0:
-            decoder = {0: "runs (k_stream_runs)", 1: "sweep (k_stream_sweep)",
+            decoder = {0: "runs (k_stream_runs)",
                        2: "runs (k_stream_runs, 512-thread workgroups, 64 KiB segments)",
                        3: "lattice (k_stream_lattice)"}.get(int(pol[4]) & 3)
 
@@ -715,25 +716,18 @@ def main():
                  "cyc_pro_fill", "cyc_pro_scan", "cyc_pro_publish", "dense_no_entry", "dense_chase_fail",
                  "dense_mismatch", "dense_overflow", "giveups", "bridges", "steal_requests", "steals",
                  "stolen_segments", "cyc_dense_validate", "cyc_rows", "cyc_serial_chase",
-                 "sweep_rechased", "sweep_pred_fail", "cyc_sweep_lookback", "cyc_sweep_scan", "cyc_sweep_spec",
-                 "sweep_slow_path", "sweep_scanned", "cyc_sweep_undecided"]
+                 "lattice_entries", "s41", "s42", "s43", "s44", "s45", "cyc_stride_pass", "s47"]
         for _ in range(2):
             dec.opts |= _lib.OPT_STATS
             dec.decode(bufs[0], cap=0, count=False, carry=False)
             dec.opts &= ~_lib.OPT_STATS
             out = (C.c_uint64 * _lib.NSTATS)()
             dec.ctx.L.xyws_debug_stats(dec.ctx.h, C.c_void_p(stream.cuda_stream), out)
-        if decoder and decoder.startswith("sweep"):  # (the sweep's own timing split: ST_SWT_*, per segment)
-            names[16:26] = ["cyc_claim_wait", "cyc_phase_a", "cyc_phase_b", "cyc_data_barrier", "cyc_data_load",
-                            "cyc_records", "cyc_data_store", "cyc_data_fill", "cyc_iteration", "cyc_predict"]
-        else:
-            names[46] = "cyc_stride_pass"
         st = {k: v for k, v in zip(names, list(out))}
-        nrun = max(1, (st["dense_passes"] if decoder and decoder.startswith("sweep") else st["runs"] + 1))
+        nrun = max(1, st["runs"] + 1)
         for k in list(st):
             if k.startswith("cyc_"):
-                per = "us_per_segment_" if decoder and decoder.startswith("sweep") else "us_per_run_"
-                st[k.replace("cyc_", per)] = round(st.pop(k) / nrun / 2100.0, 3)
+                st[k.replace("cyc_", "us_per_run_")] = round(st.pop(k) / nrun / 2100.0, 3)
         print(json.dumps({"stats": st}), flush=True)
 
     # parity after the timed region: every copy against the reference digest

@@ -1,4 +1,4 @@
-"""The decoder choice across configs on one stream (tests/test_gpu_sweep.py::
+"""The decoder choice across configs on one stream (tests/test_gpu_choice.py::
 test_decoder_choice_follows_the_frames, timed): c3, c3, c4, c4, c4, each call's
 HIP-event time and the decoder that served it. Run under
 `rocprofv3 --kernel-trace` to split a call into its kernels.

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 PMC passes of the bench into profiles/pmc_traffic.json.
 
-HBM traffic per launch of the decoder kernel the timed steps ran (k_stream_sweep or k_stream_runs), per MI355X_MICROARCH.md §HBM: gfx950's
+HBM traffic per launch of the decoder kernel the timed steps ran (k_stream_lattice or k_stream_runs), per MI355X_MICROARCH.md §HBM: gfx950's
 FETCH_SIZE reports half the bytes of wide coalesced streaming reads (doubled
 here); WRITE_SIZE reads the bytes exactly for 16-B-per-lane stores. Both
 counters are in KiB. Usage: pmc_summary.py FETCH_DIR WRITE_DIR KEY PROFILE [OUT]
@@ -18,11 +18,11 @@ import sys
 def per_launch(d, counter, kernel=None):
     """Average counter value per launch of `kernel` (a name substring); by
     default the decoder kernel (k_stream_lattice / k_stream_runs /
-    k_stream_sweep) of the last dispatches, i.e. the one the timed steps ran
+    k_stream_lattice) of the last dispatches, i.e. the one the timed steps ran
     (the decoder choice serves the first calls, before the first one has
     finished, with the run decoder); after a lattice launch the run decoder
     that follows it reads the redirect record and exits: the lattice's counts."""
-    names = ("k_stream_lattice", "k_stream_runs", "k_stream_sweep")
+    names = ("k_stream_lattice", "k_stream_runs")
     vals, last, prev = {}, None, None
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         rows = list(csv.DictReader(open(f)))

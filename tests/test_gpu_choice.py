@@ -1,0 +1,80 @@
+"""The decoder choice of xyws_decode_stream (stream_decode_fused), through the
+C-ABI: which decoder serves a call follows what the previous call on the same
+stream found (the policy words its finisher publishes), and every call's bytes,
+count and carry are the reference's whichever decoder ran
+(tests/golden/configs.json, from the real reference headers).
+"""
+import ctypes as C
+
+import pytest
+
+from test_gpu_parity import dev_digest, tools_batch
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ws():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from xynet_amd import websocket
+    return websocket
+
+
+def _policy(dec):
+    out = (C.c_uint64 * 5)()
+    stream = torch.cuda.current_stream()
+    assert dec.ctx.L.xyws_debug_policy(dec.ctx.h, C.c_void_p(stream.cuda_stream), out) == 0
+    return list(out)
+
+
+def test_decoder_choice_follows_the_frames(ws):
+    """The decoder choice (stream_decode_fused): the lattice decoder first when
+    the previous call on the stream found frames of one size (>= 128 B, policy
+    word 4 = 3), the run decoder otherwise (0, or 2 in 512-thread workgroups
+    after regular frames under 2 KiB). An irregular batch after regular ones
+    goes to the lattice decoder, which hands it to the run decoder at its first
+    size change: its time stays that of the run decoder alone (the decoder-
+    choice cliff of round 3 was 7x: the retired sweep decoder scanning every segment).
+    Every call is checked against the reference's digests, whichever decoder
+    ran."""
+    from xynet_amd import _lib
+    seq = [("c3_bin_64k", 0), ("c3_bin_64k", 0), ("c3_bin_64k", 0), ("c4_mixed", 0), ("c4_mixed", 0),
+           ("c4_mixed", 0), ("c2_bin_256", 0), ("c2_bin_256", 0), ("c3_bin_64k", _lib.OPT_RUNS)]
+    dec = ws.frame_decoder()
+    used, pols, ms = [], [], []
+    bufs = {}
+    for name, extra in seq:
+        if name not in bufs:
+            bufs.clear()
+            torch.cuda.empty_cache()
+            bufs[name] = [tools_batch(name), 0]
+        (buf, c), k = bufs[name]
+        dec.opts = extra
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        r = dec.decode(buf, cap=0, count=True, carry=False)
+        b.record()
+        torch.cuda.synchronize()
+        ms.append(a.elapsed_time(b))
+        bufs[name][1] = k + 1
+        assert r.nframes == c["decoded_frames"], name
+        assert dev_digest(buf) == (c["out_digest"] if (k + 1) % 2 else c["in_digest"]), (name, k)
+        assert dec.ctx.last_device_error() == 0
+        p = _policy(dec)
+        used.append(p[4])
+        pols.append(p)
+    # c3: regular 64 KiB frames (65 550 B with the header): the lattice decoder
+    assert pols[1][2] == pols[1][3] == 65550
+    assert used[1] == 3 and used[2] == 3
+    # the first c4 call after c3 goes to the lattice decoder and is handed to
+    # the run decoder at its second frame: the run decoder's statistics...
+    assert used[3] in (0, 2) and pols[3][2] < pols[3][3]
+    # ...and the run decoder's time (c4 alone on the run decoder: calls 4, 5)
+    assert ms[3] <= 1.25 * min(ms[4], ms[5]) + 0.05, ms
+    assert used[4] in (0, 2) and used[5] in (0, 2)
+    # after c4's irregular frames: the run decoder for c2, then the lattice
+    assert used[6] in (0, 2) and pols[6][2] == pols[6][3] == 264 and used[7] == 3
+    assert used[8] in (0, 2)                      # XYWS_OPT_RUNS forces the run decoder

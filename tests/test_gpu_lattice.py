@@ -23,7 +23,7 @@ import pytest
 
 import streams
 from test_gpu_parity import carry_list, dev_bytes, frames_list, host, torch
-from test_gpu_sweep import _policy
+from test_gpu_choice import _policy
 
 pytestmark = pytest.mark.gpu
 

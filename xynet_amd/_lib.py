@@ -25,19 +25,13 @@ OPT_WG1024 = 0x8000        # the run decoder's default geometry, whatever the ge
 OPT_TEST_GIVEUP = 0x100000
 OPT_STEAL = 0x400000
 OPT_TEST_STEAL = 0x800000
-OPT_SWEEP = 0x1000000      # the sweep decoder (segment claiming) instead of the run decoder
-OPT_TEST_SPEC = 0x2000000  # sweep decoder tests: forced mis-speculation
 OPT_RUNS = 0x80000000      # the run decoder whatever the decoder choice would take
 OPT_LATTICE = 0x400        # the lattice decoder first (the run decoder after it takes what it leaves)
 OPT_NO_LATDEC = 0x800      # never the lattice decoder
 # debug stats indices (xyws_stream.hip)
 ST_RUNS, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRAMES = range(8)
 ST_GIVEUP, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS = 32, 33, 34, 35, 36
-# sweep decoder: segments re-chased from the entering state, with nothing to
-# decode (a partial header), deferred to the repair walk; look-back / scan /
-# speculation cycles; scan windows
-ST_SW_APPLY, ST_SW_NOTHING, ST_SW_TLB, ST_SW_TSCAN, ST_SW_TSPEC, ST_SW_DEFER, ST_SW_WIN = range(40, 47)
-ST_P_LATTICE = 40  # run decoder: runs whose entry the lattice gave (find_entry; the sweep's ST_SW_APPLY slot)
+ST_P_LATTICE = 40  # run decoder: runs whose entry the lattice gave (find_entry)
 ERRORS = {-1: "invalid argument", -2: "HIP runtime error", -3: "device allocation failed",
           -4: "scratch capacity exceeded", -5: "device-side error", -6: "not complete yet"}
 

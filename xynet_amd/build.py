@@ -36,20 +36,39 @@ def _stale(out, srcs):
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+OBJ = os.path.join(PKG, ".build")  # per-source objects (git- and gpurun-ignored)
+
+
+def _run(cmd, what, verbose):
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {what}:\n{r.stdout}\n{r.stderr}")
+    if verbose and r.stderr.strip():
+        print(r.stderr)
+
+
 def build(force=False, verbose=False, extra=None):
+    """Each source compiles to its own object in parallel (the stream decoder
+    alone takes about a minute), then one hipcc link per library."""
+    from concurrent.futures import ThreadPoolExecutor
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    os.makedirs(OBJ, exist_ok=True)
+    cflags = [f for f in COMMON if f != "-shared"] + (extra or [])
+    jobs = []
     for name, srcs in TARGETS.items():
         out = os.path.join(PKG, name)
         if not force and not _stale(out, srcs):
             continue
-        cmd = [hipcc] + COMMON + (extra or []) + [os.path.join(CSRC, s) for s in srcs] + ["-o", out]
-        if verbose:
-            print(" ".join(cmd))
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"hipcc failed for {name}:\n{r.stdout}\n{r.stderr}")
-        if verbose and r.stderr.strip():
-            print(r.stderr)
+        objs = [os.path.join(OBJ, os.path.splitext(s)[0] + ".o") for s in srcs]
+        jobs.append((name, out, srcs, objs))
+    compile_cmds = [([hipcc] + cflags + ["-c", os.path.join(CSRC, s), "-o", o], s)
+                    for _, _, srcs, objs in jobs for s, o in zip(srcs, objs)]
+    with ThreadPoolExecutor(max_workers=min(8, max(1, len(compile_cmds)))) as ex:
+        list(ex.map(lambda c: _run(c[0], c[1], verbose), compile_cmds))
+    for name, out, _, objs in jobs:
+        _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC"] + objs + ["-o", out], name, verbose)
     build_cpp_tests(hipcc, force=force, verbose=verbose)
     return [os.path.join(PKG, n) for n in TARGETS]
 

@@ -63,6 +63,7 @@ enum {
   LW_BRK = 2,      // ~(earliest failing lattice index) of this call, 0 = none (reset by the finisher)
   LW_UNMASK = 3,   // xyws_unmask's claim counter pair (u32 claims, u32 done; reset by its last workgroup)
   LW_W = 4,        // the decided prefix: every segment below it has published its result (reset by the finisher)
+  LW_LOOPS = 5,    // workgroups whose segment loop has ended (reset by the finisher)
   LW_REDIR = 8,    // redirect record for the run decoder: [0] state, [1] p, [2] frames before p
   LW_RCARRY = 16,  // the carry the run decoder starts from at p (8 words)
   LW_STAT = 32     // per segment: (E << 2) | LS_*
@@ -284,6 +285,7 @@ XYWS_DEV void lat_finish(const run_params& P, lat_lds<G>& L) {
   uint32_t* cnt = reinterpret_cast<uint32_t*>(P.lat + LW_CNT);
   st_store(P.lat + LW_BRK, 0);
   st_store(P.lat + LW_W, 0);
+  st_store(P.lat + LW_LOOPS, 0);
   __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   st_store(P.lat + LW_EPOCH, L.E);
@@ -457,7 +459,7 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
   // wait for it at once) and loads the covering header and the bytes after
   // it; then every data wave its rows, the youngest loads (the fill waits for
   // them, and so for everything before them)
-  auto issue = [&](uint32_t s, bool claim) {
+  auto issue = [&](uint32_t s, bool claim, bool rows) {
     if constexpr (DT) {
       if (wave == CW) {
         if (lane == 0) {
@@ -468,16 +470,18 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
         }
         cx = lat_ctrl_load(P, s, G::SEG, X0, F, kmax, tid);
       }
-      const __amdgpu_buffer_rsrc_t rs = lat_rsrc(P, (uint64_t)s * G::SEG, G::SEG);
+      if (rows) {
+        const __amdgpu_buffer_rsrc_t rs = lat_rsrc(P, (uint64_t)s * G::SEG, G::SEG);
 #pragma unroll
-      for (uint32_t k = 0; k < IO::K; k++)
-        e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, IO::valid(wave, k) ? lane * 16u : OOB,
-                                                     IO::row(wave, k) * 1024u, AUX_NT);
+        for (uint32_t k = 0; k < IO::K; k++)
+          e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, IO::valid(wave, k) ? lane * 16u : OOB,
+                                                       IO::row(wave, k) * 1024u, AUX_NT);
+      }
     }
   };
   if (DT && cur != NONE32) {
     const uint32_t a0 = ahead;
-    issue(cur, false);
+    issue(cur, false, true);
     ahead = a0;  // (claimed at the start)
     // K dropped stores (out-of-range offset, no traffic) after the first
     // loads, as after every later segment's: the fill's waits then count the
@@ -548,7 +552,7 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
         }
         L.tab[0] = c;
       }
-      if (nxt != NONE32) issue(nxt, !L.quit);  // (in flight through the checks, the look-back and the stores)
+      if (nxt != NONE32) issue(nxt, !L.quit, true);  // (in flight through the checks, the look-back and the stores)
       // lattice points in the segment: k in [ka, kz), each checked by one data lane
       const uint32_t nlw = (P.opts & XYWS_OPT_LATX_NOWORK) ? 0u : nl;  // (timing experiment)
       for (uint32_t i = dl; i < nlw; i += NDL) {
@@ -591,7 +595,7 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
     // lattice stores past its failing point and the end-of-work check undoes
     // it)
     const bool blind = (P.opts & XYWS_OPT_TEST_LATSPEC) != 0;
-    const bool gate = it == 0 && !blind;
+    const bool gate = it == 0 && !blind && !(P.opts & XYWS_OPT_LAT_NOGATE);
     if (CT && tid < 64) {
       // the segment's own result, published while the data waves store
       // (completed before the result is published; nothing to raise when an
@@ -775,13 +779,27 @@ XYWS_DEV void lat_undo(const run_params& P, const lat_lds<G>& L, uint32_t tid, u
       m.z |= en.z & range_mask32(a + 8, en.x, en.y);
       m.w |= en.z & range_mask32(a + 12, en.x, en.y);
     }
+    if (a >= from && a >= lo_r && a + 16u <= top) {
+      // a whole chunk: four dwords (agent scope: past this CU's caches, which
+      // may hold the bytes as loaded); bytes under a zero mask (headers) are
+      // written back unchanged (no other writer runs: the run decoder comes
+      // after this kernel in the stream)
+      uint32_t* q = reinterpret_cast<uint32_t*>(P.base + ss + a);
+      const uint32_t mm[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        if (!mm[i]) continue;
+        const uint32_t v = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(q + i, v ^ mm[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;
+    }
 #pragma unroll
     for (uint32_t b = 0; b < 16; b++) {
       const uint32_t y = a + b;
       const uint32_t mw = b < 4 ? m.x : b < 8 ? m.y : b < 12 ? m.z : m.w;
       const uint8_t kbyte = (uint8_t)(mw >> (8u * (b & 3u)));
       if (kbyte && y >= from && y >= lo_r && y < top) {
-        // (agent scope: past this CU's caches, which may hold the bytes as loaded)
         uint8_t* q = P.base + ss + y;
         const uint8_t v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(q, (uint8_t)(v ^ kbyte), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -799,7 +817,11 @@ __attribute__((amdgpu_waves_per_eu(G::NT * G::WPC >= 256 ? G::NT * G::WPC / 256 
   const uint32_t tid = threadIdx.x;
   uint32_t* cnt = reinterpret_cast<uint32_t*>(P.lat + LW_CNT);
   uint32_t ahead = NONE32;  // claim lane: the segment claimed one iteration ahead
-  if (tid == IO::CLAIM) {
+  // (the prologue: the control lane's dependent round trips — the epoch and
+  // the carry, the first header, two lattice points. Issuing the static first
+  // segment's rows before it measured no faster: c1 0.1110 vs 0.1102 ms, c2
+  // 0.1245 vs 0.1246, same box, r05d)
+  if (tid == 0) {
     L.E = st_load(P.lat + LW_EPOCH) + 1;
     const xyws_carry* cz = P.cin_user ? P.cin_user : &k_zero_carry;
     uint64_t c0 = 0;
@@ -812,6 +834,40 @@ __attribute__((amdgpu_waves_per_eu(G::NT * G::WPC >= 256 ? G::NT * G::WPC / 256 
       if (!h.hlen || F < LAT_FMIN || F > LAT_FMAX) na = 1;
       else kmax = (P.hi - S0.X + F - 1) / F;
     }
+    // Lattice points 1 and 2 (X0 + F, X0 + 2F) from memory before anything is
+    // stored: a batch whose frames change size there (an irregular batch after
+    // regular ones) goes to the run decoder whole at once, at the cost of this
+    // workgroup's first rows (not a gated first round of every workgroup).
+    // (Not in the blind test mode, whose breaks at frame 1 exercise the undo.)
+    if (!na && kmax > 1 && !(P.opts & (XYWS_OPT_TEST_LATSPEC | XYWS_OPT_LATX_NOCHK))) {
+      const uint64_t dl = (P.hi + 3) & ~3ull;
+      uint32_t r[2][5];
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const uint64_t a = (S0.X + (j + 1) * F) & ~3ull;
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          const uint64_t q = a + 4 * i;
+          r[j][i] = (j == 0 || kmax > 2) && q < dl ? *reinterpret_cast<const uint32_t*>(P.base + q) : 0u;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const uint64_t k = j + 1;
+        if (k >= kmax) break;
+        const uint64_t x = S0.X + k * F;
+        const uint32_t sh = (uint32_t)(x & 3);
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) w[i] = __builtin_amdgcn_alignbyte(r[j][i + 1], r[j][i], sh);
+        const uint64_t room = P.hi - x;
+        const hdr_info h = parse_header_words(w, room < 16 ? (uint32_t)room : 16u);
+        const bool last = k + 1 == kmax;
+        const uint64_t fend = h.hlen ? sat_add(x + h.hlen, h.plen) : x;
+        const bool ok = h.hlen ? ((uint64_t)h.hlen + h.plen == F && h.plen < F) || (last && fend >= P.hi) : last;
+        if (!ok) na = 1;
+      }
+    }
     L.S0 = S0;
     L.c0 = c0;
     L.X0 = S0.X;
@@ -820,16 +876,13 @@ __attribute__((amdgpu_waves_per_eu(G::NT * G::WPC >= 256 ? G::NT * G::WPC / 256 
     L.na = na;
     L.quit = 0;
     L.nsl = 0;
-    L.cur = NONE32;
-    if (!na) {
-      // the first round is static (segment b, then b + grid: every
-      // workgroup's first segment, the one its gate holds, is among the
-      // first grid segments, so no gate waits on a segment that waits itself),
-      // then claims from the counter offset by 2 * grid (lat_loop)
-      L.cur = blockIdx.x < P.nseg ? blockIdx.x : NONE32;
-      ahead = blockIdx.x - gridDim.x;  // (+ 2 * grid at its use: b + grid)
-    }
+    // the first round is static (segment b, then b + grid: every workgroup's
+    // first segment, the one its gate holds, is among the first grid
+    // segments, so no gate waits on a segment that waits itself), then claims
+    // from the counter offset by 2 * grid (lat_loop)
+    L.cur = !na && blockIdx.x < P.nseg ? blockIdx.x : NONE32;
   }
+  if (tid == IO::CLAIM) ahead = blockIdx.x - gridDim.x;  // (+ 2 * grid at its use: b + grid)
   __syncthreads();
   if (!L.na) {
     if constexpr (IO::CTRL) {
@@ -842,6 +895,42 @@ __attribute__((amdgpu_waves_per_eu(G::NT * G::WPC >= 256 ? G::NT * G::WPC / 256 
       lat_loop<G, LR_ALL>(P, L, tid, ahead);
     }
     __syncthreads();
+    // A failing point known when this workgroup's work ends: wait until every
+    // workgroup's segment loop has ended (LW_BRK final: a segment raises it
+    // before it publishes, and no segment is decoded after the loops end; no
+    // loop waits for anything here) and undo this workgroup's own speculative
+    // stores past it, all workgroups in parallel (a break near the batch start
+    // after an ungated first round: up to a segment per workgroup). A break
+    // raised later than that is the finisher's, from the dumped lists
+    // (emptied here once undone).
+    // (L.quit: a failing point this workgroup knew of, its own or LW_BRK as
+    // read during its loop: no extra load when none was)
+    if (tid < 64) {
+      uint64_t b = 0;
+      if (tid == 0) __hip_atomic_fetch_add(P.lat + LW_LOOPS, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (L.quit && L.nsl) {
+        for (uint32_t it = 0; uniform64(st_load(P.lat + LW_LOOPS)) < gridDim.x; it++) {
+          if (it >= (1u << 20)) {
+            if (tid == 0) atomicOr(P.head + 1, 2u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(8);
+        }
+        b = uniform64(st_load(P.lat + LW_BRK));
+      }
+      if (tid == 0) L.kbf = b && L.nsl ? ~b : NONE;
+    }
+    __syncthreads();
+    const uint64_t kb = L.kbf;
+    if (kb != NONE) {
+      const uint32_t n = L.nsl;
+      for (uint32_t j = 0; j < n; j++)
+        if (kb < L.sl_k[j]) lat_undo<G>(P, L, tid, L.sl_seg[j], L.sl_k[j], kb);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) L.nsl = 0;
+      __syncthreads();
+    }
     lat_dump_list<G>(P, L, tid);
   }
   // end of the workgroup: the last one to finish writes the call's outputs

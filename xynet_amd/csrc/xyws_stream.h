@@ -13,13 +13,10 @@ struct stream_scratch {
   int ncu;              // compute units of the context's device (runs per launch)
   void* fmem;           // frame-start lists for descriptor emission (grown with the caller's cap)
   uint64_t fbytes;
-  void* smem;           // sweep decoder: per-segment granules, records and flag bitmap
-  uint64_t sbytes;
-  uint64_t max_segs;    // segments smem covers
   // decoder choice: pinned host words the finisher of every call writes
   // ({epoch, batch bytes, smallest, largest last-frame size, decoder}) and
   // their device address; null when the pinned allocation failed (then the
-  // run decoder serves every call that does not ask for the sweep)
+  // run decoder serves every call)
   volatile uint64_t* pol_h;
   uint64_t* pol_d;
   void* lmem;           // lattice decoder: scratch words + one result word per segment
@@ -60,13 +57,12 @@ int stream_scratch_unmask_counter(stream_scratch* s, bool capturing, uint32_t** 
 #define XYWS_OPT_NO_LATTICE 0x200000u   // experiment (run decoder): no lattice passes (row table and walk only)
 #define XYWS_OPT_STEAL 0x400000u       // work stealing between runs (off by default: measured no faster on c1-c4)
 #define XYWS_OPT_TEST_STEAL 0x800000u  // tests: stealing on, every fourth run starts late, pieces of 1 segment and up
-#define XYWS_OPT_SWEEP 0x1000000u      // the sweep decoder (segment claiming) instead of the run decoder;
-                                       // calls without descriptors only (measured slower on c1-c4, opt-in)
-#define XYWS_OPT_SW_LATEPF 0x4000000u  // experiment (sweep): the next segment's loads issued after the entry scan
-#define XYWS_OPT_SW_FULLSCAN 0x8000000u  // experiment (sweep): scan the whole segment for an entry, not its first window
-#define XYWS_OPT_SWX_NOVAL 0x10000000u  // timing experiments only (wrong results possible): no deferred checks
-#define XYWS_OPT_SWX_NOREC 0x20000000u  // timing experiments only: no segment records
-#define XYWS_OPT_SW_LOADWAIT 0x40000000u  // experiment (sweep): the next segment's loads land before the stores issue
+#define XYWS_OPT_LAT_NOGATE 0x1000000u  // (set by stream_decode_fused only) the lattice decoder without the
+                                        // first-segment gate: the previous call on the stream was the lattice's
+#define XYWS_OPT_LAT_GATE 0x2000000u    // experiment (lattice decoder): the first-segment gate whatever the
+                                        // previous call found
+#define XYWS_OPT_LATX_NOCHK 0x8000000u  // experiment (lattice decoder): no check of lattice points 1 and 2 up front
+// (0x10000000..0x40000000: free)
 #define XYWS_OPT_RUNS 0x80000000u     // the run decoder, whatever the decoder choice would take
 #define XYWS_OPT_LATTICE 0x400u      // the lattice decoder first, whatever the decoder choice would take
 #define XYWS_OPT_NO_LATDEC 0x800u    // never the lattice decoder
@@ -79,8 +75,6 @@ int stream_scratch_unmask_counter(stream_scratch* s, bool capturing, uint32_t** 
                                     // the checks and the XOR (its data path and control alone)
 #define XYWS_OPT_REDIRECT 0x2000u    // (set by stream_decode_fused only) the run decoder after the lattice decoder:
                                      // it reads the lattice's redirect record first
-#define XYWS_OPT_TEST_SPEC 0x2000000u  // tests (sweep decoder): segments 1, 4, 7, ... report no entry, segments
-                                       // 2, 5, 8, ... speculate one byte late (look-back fix-ups, repair walk)
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
                         const xyws_carry* cin, xyws_carry* cout, xyws_frame* frames, uint64_t cap,
                         uint64_t* nframes, uint32_t opts, hipStream_t stream);

@@ -104,15 +104,12 @@ constexpr uint32_t S_HDRCARRY = 8;   // covering frame's header began in the pre
 constexpr uint32_t S_PARTCARRY = 16; // the carried partial header is still incomplete
 constexpr uint32_t S_CUT = 32;       // header at X crosses the write limit (left to the repair)
 
-template <uint32_t NT_, uint32_t CH_, uint32_t WPE_, bool PD_ = false>
+template <uint32_t NT_, uint32_t CH_, uint32_t WPE_>
 struct geom {
   // threads, 16-byte chunks per thread, waves per SIMD the decode kernel must
   // fit (register budget 512 / WPE)
   static constexpr uint32_t NT = NT_, CH = CH_, SEG = NT_ * CH_ * 16, WPE = WPE_;
-  // PADDED (the sweep decoder): the 16 bytes after the segment are in LDS too
-  // (a header starting in the segment is parsed from LDS whatever its length)
-  static constexpr bool PADDED = PD_;
-  static constexpr uint32_t SEGX = SEG + (PD_ ? 16u : 0u);
+  static constexpr uint32_t SEGX = SEG;  // (bytes of the segment readable from LDS)
   // frame-list entries per pass (one per thread: the dense pass compacts them
   // one per thread); prologue lists overlaying the frame list
   static constexpr uint32_t FCAP = NT_, SCAP = NT_ * 2, UCAP = NT_ * 2;
@@ -123,8 +120,6 @@ using G_PROD = geom<1024, 8, 4>;  // 128 KiB segments, 16 waves, one workgroup p
 using G_PROD2 = geom<512, 8, 4>;  // 64 KiB segments, 8 waves, two workgroups per CU (XYWS_OPT_WG512)
 using G_SMALL = geom<64, 1, 1>;   // 1 KiB segments, one wave (XYWS_OPT_SMALL_SEG)
 using G_MID = geom<256, 4, 4>;    // 16 KiB segments, 4 waves, four workgroups per CU (mid_preferred)
-using G_SWEEP = geom<1024, 8, 4, true>;  // the sweep decoder: 128 KiB segments
-using G_SWEEP_SMALL = geom<64, 1, 1, true>;  // the sweep decoder on 1 KiB segments (tests)
 
 struct fent {
   uint32_t start, ps, end, kw;  // segment-relative, clamped to [0, 2^32-1]
@@ -260,13 +255,7 @@ struct run_params {
   // rcap); k_stream_emit writes the descriptors from them in parallel
   uint64_t* fst;
   uint64_t rcap;
-  // sweep decoder (k_stream_sweep): segments, their published spec states
-  // (two 16-byte granules each), records (SR_WORDS x u64 each) and the bitmap
-  // of segments whose final exit differs from what they published
-  uint64_t nseg;
-  uint64_t* sgran;
-  uint64_t* srec;
-  uint64_t* sbits;
+  uint64_t nseg;  // lattice decoder: segments of the batch
   // host-visible policy slot (device address of pinned host memory; nullable):
   // written by the workgroup that finishes the call (pol_publish)
   uint64_t* pol;
@@ -326,15 +315,6 @@ struct __attribute__((aligned(16))) lds_t {
   // lattice pass (run_chain): entries 1.. start at ar_x0 + (i - 1) * ar_f
   uint32_t ar, ar_x0, ar_f;
   uint32_t nrec;   // descriptors requested: frame starts the current item recorded
-  // sweep decoder: claimed segments (current, next, claimed ahead), the spec
-  // entry and state, the entering state from the look-back, decisions; the
-  // stride prediction of the current segment (pcur, fcur) and of the next
-  // (pnx, fnx, made when it is known: the top of the segment loop)
-  uint64_t sw_cur, sw_next, sw_ahead, sw_h, sw_ref, sw_fsz, sw_pcur, sw_fcur, sw_pnx, sw_fnx, sw_vs;
-  cstate sw_spec, sw_in, sw_vU;
-  uint32_t sw_act, sw_single, sw_cnt_spec, sw_fast, sw_padok;
-  uint64_t sw_t[9];  // sweep timing split (XYWS_OPT_STATS): see ST_SWT_*
-  uint64_t sw_fsmin, sw_fsmax;  // lane 0: smallest / largest last-frame size of the segments decoded
 };
 
 // ---------------------------------------------------------------- small helpers
@@ -350,8 +330,8 @@ enum { ST_RUNS = 0, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRA
        ST_T_PRO = 16, ST_T_MAIN, ST_T_WAIT, ST_T_FILL, ST_T_CHASE, ST_T_XOR, ST_T_TAIL, ST_T_PF, ST_T_CP,
        ST_P_FILL, ST_P_SCAN, ST_P_PUB, ST_D_NOENT, ST_D_CHASE, ST_D_MISMATCH, ST_D_OVF,
        ST_GIVEUP = 32, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS, ST_D_TVAL, ST_T_ROWS, ST_T_SER,
-       ST_T_STRIDE = 46,    // (46: the sweep's ST_SW_WIN; the run decoder's stride-pass time)
-       ST_P_LATTICE = 40 }; // (40: the sweep's ST_SW_APPLY; runs whose entry the lattice gave)
+       ST_T_STRIDE = 46,    // the run decoder's stride-pass time
+       ST_P_LATTICE = 40 }; // runs whose entry the lattice gave
 XYWS_DEV void stat_add(const run_params& P, uint32_t i, uint64_t v) {
   if (stats_on(P)) atomicAdd(reinterpret_cast<unsigned long long*>(P.head + 32) + i, (unsigned long long)v);
 }
@@ -521,7 +501,7 @@ XYWS_DEV uint32_t chunk_candidates(const run_params& P, const lds_t<G>& L, uint3
   uint32_t bits = cand_nibble(v.x, v.y, unm) | (cand_nibble(v.y, v.z, unm) << 4) |
                   (cand_nibble(v.z, v.w, unm) << 8) | (cand_nibble(v.w, w4, unm) << 12);
   // headers straddling the segment end are left to the next segment's scan
-  if (!G::PADDED && a + 16 + 1 > G::SEG) bits &= (1u << (G::SEG - XYWS_MAX_FRAME_HEADER_SIZE - a + 1)) - 1u;
+  if (a + 16 + 1 > G::SEG) bits &= (1u << (G::SEG - XYWS_MAX_FRAME_HEADER_SIZE - a + 1)) - 1u;
   return bits;
 }
 
@@ -688,53 +668,6 @@ XYWS_DEV void record_start(const run_params& P, lds_t<G>& L, uint64_t self, uint
 // An all-zero carry (a decode without incoming carry).
 __device__ const xyws_carry k_zero_carry = {};
 
-// Sweep decoder: a segment's first 16 original bytes, published in two
-// granules (8 data bytes + the call's epoch flag each) right after the
-// segment is in LDS, before its workgroup writes anything: the bytes a header
-// straddling the end of the segment before it needs (the chase waits for them
-// there, sweep_pad; the repair walk reads them too).
-XYWS_DEV void sweep_orig_publish(const run_params& P, uint64_t s, uint64_t E, const u32x4& o) {
-  uint64_t* g = P.sgran + 8 * s + 4;
-  granule_store(g, (uint64_t)o.x | ((uint64_t)o.y << 32), flag_published(E));
-  granule_store(g + 2, (uint64_t)o.z | ((uint64_t)o.w << 32), flag_published(E));
-}
-// Segment s's published first bytes (lane 0; waits for them; bounded).
-XYWS_DEV u32x4 sweep_orig_wait(const run_params& P, uint64_t s, uint64_t E) {
-  const uint64_t* g = P.sgran + 8 * s + 4;
-  uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
-  for (uint32_t it = 0;; it++) {
-    granule_load(g, a0, a1);
-    granule_load(g + 2, b0, b1);
-    if (a1 == flag_published(E) && b1 == flag_published(E)) break;
-    if (it >= (1u << 20)) {
-      atomicOr(P.head + 1, 2u);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return u32x4{(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)b0, (uint32_t)(b0 >> 32)};
-}
-// The next segment's first bytes for a header straddling the end of the
-// segment at ss (lane 0): when this workgroup claimed that segment itself, no
-// one has written it (memory); else its workgroup publishes them as soon as it
-// has them (its current segment waits for nothing at or above this one: no
-// cycle).
-template <class G>
-XYWS_DEV void sweep_pad(const run_params& P, lds_t<G>& L, uint64_t ss) {
-  const uint64_t n = ss / G::SEG + 1;
-  u32x4 v = {0u, 0u, 0u, 0u};
-  if (n < P.nseg) {
-    if (n == L.sw_next) {
-      const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, n * G::SEG);
-      v = __builtin_amdgcn_raw_buffer_load_b128(rs, 0u, 0u, AUX_NT);
-    } else {
-      v = sweep_orig_wait(P, n, L.E);
-    }
-  }
-  *reinterpret_cast<u32x4*>(&L.seg[G::SEG]) = v;
-  L.sw_padok = 1;
-}
-
 // One pass of the chase over segment [ss, ss+SEG), lane 0: the frame covering
 // the pass start, then frames parsed from X, up to G::FCAP entries. Sets
 // pass_hi: the chunks below it are final for this pass.
@@ -799,11 +732,6 @@ XYWS_DEV void chase_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
     if (X >= P.hi || (S.st & (S_PARTIAL | S_CUT))) { end = true; break; }
     if (X >= lim) { done = true; break; }
     if (X >= se || n >= G::FCAP) break;
-    if constexpr (G::PADDED) {
-      // a header that may straddle the segment end: the bytes after it as the
-      // next segment held them before anyone wrote (sweep_pad)
-      if (X + XYWS_MAX_FRAME_HEADER_SIZE > se && !L.sw_padok) sweep_pad<G>(P, L, ss);
-    }
     const hdr_info h = hdr_at(P, L, ss, X, lim);
     if (!h.hlen) {
       // incomplete: at the batch end (carry) or at the successor's write start
@@ -2863,1233 +2791,7 @@ __global__ void k_stream_empty(const xyws_carry* cin, xyws_carry* cout, uint64_t
   }
 }
 
-// ================================================================ sweep decoder
-// k_stream_sweep: the decoder for calls that ask for no descriptors (the
-// headline path). Every 128 KiB SEGMENT of the batch is a unit of work that
-// workgroups claim in batch order from one counter (one claim ahead, so the
-// claimed segment's loads fly while the current one is decoded): all CUs
-// sweep the batch together and finish within about one segment of each
-// other, instead of each CU streaming its own fixed range and the slowest XCD
-// setting the call's end (scripts/bw_probe6.hip: static ranges end over a
-// 100 us spread; segment claims hold 6.4 TB/s to the end).
-//
-// A segment needs the state of the chain entering it (which frame covers its
-// first bytes, where the next frame starts): the chain is a linked list
-// through the batch (websocket_frame_header.h:305-385). Per segment:
-//  1. speculate: the earliest position whose chain of headers is plausible
-//     for a client stream (sweep_scan), the chase from there through the
-//     segment (and, through the 16 bytes after it held in LDS, any header
-//     that starts in it) gives a speculative EXIT state, published at once in
-//     two 16-byte epoch-tagged granules: it never waits for anything;
-//  2. look back: the state entering the segment is the published exit of the
-//     nearest earlier segment that published one (segments with no plausible
-//     start publish none: a frame covers them); the wait is for a neighbour's
-//     speculation only, never for a chain of them;
-//  3. decode: when the entering state's next frame start is the speculated
-//     entry (the usual case) the speculative frame list is the exact one and
-//     the whole segment (its first bytes with the entering frame's key) is
-//     XORed and stored once; otherwise the segment is re-chased from the
-//     entering state before anything is stored, from its LDS copy;
-//  4. a segment whose final exit differs from what it published (a
-//     mis-speculation whose chains did not merge), or that could not decode
-//     (its entering state lies before it: a frame start in a segment that
-//     published none), is flagged; the workgroup finishing the call walks the
-//     flagged segments in order, undoing each affected segment (replaying its
-//     own decode: XOR is an involution, a chain never writes its own header
-//     bytes) and redoing it from the exact state, until the states agree again.
-// By induction from segment 0 (exact: the batch start and the carry), every
-// unflagged segment is exact. Speculation decides speed only.
-//
-// Records (SR_WORDS x u64 per segment, for the finisher): the entering state
-// used (U), the final exit (F), the speculated entry, the frame count, the
-// segment's first 16 original bytes (the repair's view of the bytes after the
-// previous segment) and flags.
-enum { SR_U = 0, SR_F = 5, SR_H = 10, SR_CNT = 11, SR_WORDS = 12 };
-constexpr uint64_t XCLAMP = (1ull << 46) - 1;  // published positions (batches are below 2^46 bytes)
-constexpr uint32_t SPIN_SW = 1u << 20;          // bounded look-back polls (~1 s)
-// sweep timing split (shader clocks, summed over workgroups): tid 0 (the
-// control wave) waiting for its claim at the fill, its phase A, its phase B;
-// tid 64 (a data wave) from its loads' issue to the phase barrier, waiting for
-// its loads, issuing its stores, from the loop top to its fill's end, and the
-// whole iteration (ST_T_XOR stays the record/epilogue time)
-enum { ST_SWT_CLAIMW = 16, ST_SWT_A, ST_SWT_B, ST_SWT_DBAR, ST_SWT_DLOAD, ST_SWT_DSTORE = 22, ST_SWT_DFILL,
-       ST_SWT_ITER, ST_SWT_PRED };  // (PRED: phase A up to the entering state)
-XYWS_DEV uint64_t swt_now(const run_params& P) { return stats_on(P) ? __builtin_amdgcn_s_memtime() : 0; }
-enum { ST_SW_APPLY = 40, ST_SW_NOTHING, ST_SW_TLB, ST_SW_TSCAN, ST_SW_TSPEC, ST_SW_DEFER, ST_SW_WIN, ST_SW_TUND };
-// sweep actions
-enum { SW_REUSE = 0, SW_APPLY = 1, SW_NOTHING = 2 };
-
-XYWS_DEV uint64_t tag13(uint64_t E) { return E & 0x1FFFull; }
-XYWS_DEV uint64_t clampX(uint64_t x) { return x < XCLAMP ? x : XCLAMP; }
-XYWS_DEV bool same_state(const cstate& a, const cstate& b) {
-  return clampX(a.X) == clampX(b.X) && a.cov_ps == b.cov_ps && a.cov_start == b.cov_start &&
-         a.cov_kw == b.cov_kw && a.st == b.st;
-}
-
-// Publish segment s's speculative exit (lane 0): granule 1 (the state) first,
-// granule 0 (epoch flag, X, has-state) second; every 8-byte half carries the
-// call's epoch (word 0 whole, the others its low 13 bits), so a reader never
-// takes a previous call's or a torn granule.
-XYWS_DEV void sweep_publish(const run_params& P, uint64_t s, uint64_t E, bool has, const cstate& S) {
-  const uint64_t t = tag13(E);
-  uint64_t* g = P.sgran + 8 * s;
-  if (has)
-    granule_store(g + 2, (S.cov_start & XCLAMP) | (((S.cov_ps - S.cov_start) & 15ull) << 46) | (t << 50),
-                  (uint64_t)S.cov_kw | ((uint64_t)(S.st & 63u) << 32) | (t << 38));
-  granule_store(g, flag_published(E), clampX(S.X) | (t << 46) | ((has ? 1ull : 0ull) << 59));
-}
-
-// Segment s's publication as this lane sees it: 0 not yet (or torn), 1
-// published without a state, 2 published with the state S.
-XYWS_DEV uint32_t sweep_peek(const run_params& P, uint64_t s, uint64_t E, cstate& S) {
-  const uint64_t* g = P.sgran + 8 * s;
-  u32x4 a, b;
-  asm volatile("global_load_dwordx4 %0, %2, off sc1\n\tglobal_load_dwordx4 %1, %2, off offset:16 sc1\n\t"
-               "s_waitcnt vmcnt(0)"
-               : "=&v"(a), "=&v"(b) : "v"(g) : "memory");
-  const uint64_t w0 = a.x | ((uint64_t)a.y << 32), w1 = a.z | ((uint64_t)a.w << 32);
-  const uint64_t w2 = b.x | ((uint64_t)b.y << 32), w3 = b.z | ((uint64_t)b.w << 32);
-  const uint64_t t = tag13(E);
-  if (w0 != flag_published(E) || ((w1 >> 46) & 0x1FFFull) != t) return 0;
-  if (!((w1 >> 59) & 1ull)) return 1;
-  if (((w2 >> 50) & 0x1FFFull) != t || ((w3 >> 38) & 0x1FFFull) != t) return 0;
-  S.X = w1 & XCLAMP;
-  S.cov_start = w2 & XCLAMP;
-  S.cov_ps = S.cov_start + ((w2 >> 46) & 15ull);
-  S.cov_kw = (uint32_t)w3;
-  S.cov_key = 0;
-  S.st = (uint32_t)(w3 >> 32) & 63u;
-  S.pad = 0;
-  return 2;
-}
-
-XYWS_DEV uint64_t shfl64(uint64_t v, uint32_t l) {
-  return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, (int)l) |
-         ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)l) << 32);
-}
-
-// The state entering segment s > 0 at ss (wave 0, every lane; the result in
-// every lane): the published exit of the NEAREST earlier segment that has
-// published, provided its next frame start is not before ss (segments between
-// it and s that have not published yet lie inside its last frame, whatever
-// they publish), or the batch ended in a header there (S_PARTIAL); when the
-// next frame starts before ss, a nearer segment holds it and will publish:
-// wait. Lane i looks at segment j-1-i, 64 at a time. Segments are claimed
-// only by running workgroups, and the lowest unpublished segment waits for
-// nothing unpublished, so the wait ends; the bound only reports a bug (device
-// error bit 2) and returns false.
-XYWS_DEV bool sweep_lookback(const run_params& P, uint64_t s, uint64_t ss, uint64_t E, uint32_t lane,
-                             cstate& out) {
-  uint64_t j = s;
-  uint32_t it = 0;
-  for (;;) {
-    cstate S;
-    S.X = 0; S.cov_ps = 0; S.cov_start = 0; S.cov_kw = 0; S.cov_key = 0; S.st = 0; S.pad = 0;
-    const bool valid = j >= 1 + (uint64_t)lane;
-    const uint32_t r = valid ? sweep_peek(P, j - 1 - lane, E, S) : 0u;
-    const uint64_t pub = __ballot(r == 2u);
-    if (pub) {
-      const uint32_t f = (uint32_t)__builtin_ctzll(pub);
-      const uint64_t X = shfl64(S.X, f);
-      const uint32_t st = (uint32_t)__shfl((int)S.st, (int)f);
-      if (X >= ss || (st & S_PARTIAL)) {
-        out.X = X;
-        out.cov_ps = shfl64(S.cov_ps, f);
-        out.cov_start = shfl64(S.cov_start, f);
-        out.cov_kw = (uint32_t)__shfl((int)S.cov_kw, (int)f);
-        out.cov_key = 0;
-        out.st = st;
-        out.pad = 0;
-        if (it && lane == 0) stat_add(P, ST_SPIN, it);
-        return true;
-      }
-    } else if (j > 64) {
-      j -= 64;  // nothing published among these 64: further back
-      continue;
-    }
-    // wait for a nearer segment
-    if (++it >= SPIN_SW) {
-      if (lane == 0) atomicOr(P.head + 1, 2u);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-    j = s;
-  }
-}
-
-// Speculative entry of the segment at ss (whole workgroup): L.best = the
-// earliest offset whose chain of KHDR headers is plausible (NONE32: none),
-// windows of NT chunks (16 KiB at 1024 lanes) one at a time, stopping at the
-// first window with a winner; every start in the segment is a candidate (its
-// header bytes past the segment are in the LDS pad). Chains that leave the
-// segment are decided through memory afterwards when they lie below the winner.
-template <class G>
-XYWS_DEV void sweep_scan(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid, bool unm, uint32_t nwin) {
-  if (tid == 0) { L.ucnt = 0; L.ovf = 0; L.ccnt = 0; L.best = 0xFFFFFFFFu; }
-  const uint64_t rel_hi = P.hi - ss;
-  const uint32_t qlim = rel_hi < G::SEG ? (uint32_t)rel_hi : G::SEG;
-  uint32_t done = 0;  // survivors already checked
-  __syncthreads();
-  for (uint32_t k = 0; k < nwin && k < G::CH; k++) {
-    const uint32_t a = (k * G::NT + tid) * 16u;
-    uint32_t c = 0;
-    if (a < qlim) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(L.seg + a);
-      const uint32_t w4 = *reinterpret_cast<const uint32_t*>(L.seg + a + 16);
-      c = (cand_bytes(v.x, v.y, unm) >> 7) | (cand_bytes(v.y, v.z, unm) >> 6) | (cand_bytes(v.z, v.w, unm) >> 5) |
-          (cand_bytes(v.w, w4, unm) >> 4);
-      if (a + 16 > qlim) {
-        uint32_t keep = 0;
-#pragma unroll 1
-        for (uint32_t t = 0; a + t < qlim && t < 16; t++) keep |= 1u << (8u * (t & 3u) + (t >> 2));
-        c &= keep;
-      }
-    }
-    while (c) {
-      const uint32_t t = __builtin_ctz(c);
-      c &= c - 1;
-      const uint32_t pos = a + 4u * (t & 3u) + (t >> 3);
-      if (second_hop_ok<G>(P, L, ss, pos, unm)) {
-        const uint32_t slot = atomicAdd(&L.ccnt, 1u);
-        if (slot < G::SCAP) L.sl[slot] = pos;
-      }
-    }
-    __syncthreads();
-    const uint32_t n = L.ccnt;
-    if (n > G::SCAP) {
-      if (tid == 0) L.ovf = 1;
-    } else {
-      uint32_t i0 = done + tid;
-      asm volatile("" : "+v"(i0));
-      for (uint32_t i = i0; i < n; i += G::NT) {
-        const uint32_t pos = L.sl[i];
-        if (pos > __hip_atomic_load(&L.best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) continue;
-        const uint32_t r = chain_plausible(P, L, ss, ss + pos, unm, false);
-        if (r == 1u) {
-          atomicMin(&L.best, pos);
-        } else if (r == 2u) {
-          const uint32_t u = atomicAdd(&L.ucnt, 1u);
-          if (u < G::UCAP) L.ul[u] = pos;
-          else L.ovf = 1;
-        }
-      }
-    }
-    done = n;
-    __syncthreads();
-    if (L.ovf || L.best != 0xFFFFFFFFu) break;
-  }
-  if (L.ovf) {
-    // a list overflowed (e.g. a stream of 2-byte frames): each lane checks its
-    // own candidates in order, through memory, from scratch
-    __syncthreads();
-    if (tid == 0) L.best = 0xFFFFFFFFu;
-    __syncthreads();
-#pragma unroll 1
-    for (uint32_t k = 0; k < G::CH; k++) {
-      const uint32_t a = (k * G::NT + tid) * 16u;
-      uint32_t b = ss + a < P.hi ? chunk_candidates<G>(P, L, a, unm) : 0u;
-      bool hit = false;
-      while (b) {
-        const uint32_t t = __builtin_ctz(b);
-        b &= b - 1;
-        const uint32_t pos = a + t;
-        if (pos >= qlim) break;
-        if (pos > __hip_atomic_load(&L.best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { hit = true; break; }
-        if (chain_plausible(P, L, ss, ss + pos, unm, true) == 1u) {
-          atomicMin(&L.best, pos);
-          hit = true;
-          break;
-        }
-      }
-      if (hit) break;
-    }
-    __syncthreads();
-    return;
-  }
-  const uint32_t nu = L.ucnt, best = L.best;
-  if (nu) {
-    const uint64_t t0 = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
-    for (uint32_t i = tid; i < nu; i += G::NT) {
-      const uint32_t pos = L.ul[i];
-      if (pos < best) {
-        stat_add(P, ST_P_UND, 1);
-        if (chain_plausible(P, L, ss, ss + pos, unm, true) == 1u) atomicMin(&L.best, pos);
-      }
-    }
-    __syncthreads();
-    if (stats_on(P) && tid == 0) stat_add(P, ST_SW_TUND, __builtin_amdgcn_s_memtime() - t0);
-  }
-}
-
-// XOR stores of one pass over the segment at ss (whole workgroup, after the
-// row table): one 16-byte store per chunk (dropped ones to the out-of-range
-// offset), then the chunks holding a frame boundary or a write-window edge
-// (run_chain's store loop).
-template <class G>
-XYWS_DEV void store_pass(const run_params& P, const lds_t<G>& L, uint64_t ss, uint32_t tid, uint32_t nfl,
-                         uint32_t lo_c, uint32_t hi_c, uint64_t wl, uint64_t whi, uint32_t wl_r, uint32_t wh_r) {
-  const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss);
-  uint32_t edge = 0;
-  const uint32_t wave = tid >> 6;
-  const uint32_t put = boundary_chunks<G, G::CH>(
-      const_cast<lds_t<G>&>(L), L.fl, L.rt, nfl, lo_c, hi_c, wl_r, wh_r,
-      [&](uint32_t k, uint32_t& a, uint32_t& r, bool& ok) {
-        a = (k * G::NT + tid) * 16u;
-        r = k * (G::NT / 64) + wave;
-        ok = true;
-      },
-      edge);
-  u32x4 dprev = {0u, 0u, 0u, 0u};
-  uint2 rw_n = L.rt[wave];
-  u32x4 v_n = *reinterpret_cast<const u32x4*>(&L.seg[tid * 16u]);
-#pragma unroll
-  for (uint32_t k = 0; k < G::CH; k++) {
-    const uint32_t a = (k * G::NT + tid) * 16u;
-    const uint2 rw = rw_n;
-    const u32x4 v = v_n;
-    if (k + 1 < G::CH) {
-      rw_n = L.rt[(k + 1) * (G::NT / 64) + wave];
-      v_n = *reinterpret_cast<const u32x4*>(&L.seg[((k + 1) * G::NT + tid) * 16u]);
-    }
-    const uint32_t info = __builtin_amdgcn_readfirstlane(rw.x);
-    const uint32_t kw = __builtin_amdgcn_readfirstlane(rw.y);
-    u32x4 m;
-    uint32_t off;
-    if (info & ROW_FAST) {
-      m = u32x4{kw, kw, kw, kw};
-      off = tid * 16u;
-    } else if (info & ROW_SKIP) {
-      m = u32x4{0u, 0u, 0u, 0u};
-      off = OOB;
-    } else {
-      m = u32x4{0u, 0u, 0u, 0u};
-      off = ((put >> k) & 1u) ? tid * 16u : OOB;  // (boundary_chunks)
-      (void)a;
-    }
-    const u32x4 d = v ^ m;
-    __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, k * G::NT * 16u, AUX_ST);
-    // (see run_chain: the store's data registers stay live past the next store)
-    asm volatile("" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
-    dprev = d;
-  }
-  asm volatile("s_nop 1" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
-#pragma nounroll
-  while (edge) {
-    const uint32_t k = __builtin_ctz(edge);
-    edge &= edge - 1;
-    const uint32_t a = (k * G::NT + tid) * 16u;
-    uint32_t x = 0, y = nfl;
-    while (y - x > 1) {
-      const uint32_t mid = (x + y) >> 1;
-      if (L.fl[mid].start <= a) x = mid; else y = mid;
-    }
-    const u32x4 m = chunk_xor(L.fl, nfl, x, a);
-    if ((m.x | m.y | m.z | m.w) == 0u) continue;
-    if (a >= wl_r && a + 16 <= wh_r) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
-      __builtin_amdgcn_raw_buffer_store_b128(v ^ m, rs, tid * 16u, k * G::NT * 16u, AUX_ST);
-      asm volatile("s_nop 1" ::: "memory");
-      continue;
-    }
-    const uint64_t A = ss + a;
-#pragma nounroll
-    for (uint32_t t = 0; t < 16; t++) {
-      const uint64_t q = A + t;
-      const uint32_t mw = t < 4 ? m.x : t < 8 ? m.y : t < 12 ? m.z : m.w;
-      const uint8_t kb = (uint8_t)(mw >> (8u * (t & 3u)));
-      if (kb && q >= wl && q < whi) P.base[q] = L.seg[a + t] ^ kb;
-    }
-  }
-}
-
-// Sweep data path. In the production geometry wave 0 is the CONTROL wave: it
-// never loads or stores segment bytes, so its own memory operations (claims,
-// publications, look-backs, register reloads) never wait behind a segment's
-// loads or stores (vmcnt counts a wave's memory operations in issue order);
-// waves 1..15 move the segment, one 1 KiB row (one wave instruction of
-// 16-byte chunks) at a time, rows w-1, w-1+15, ... for wave w. In the
-// one-wave test geometry wave 0 does both.
-template <class G>
-struct sweep_io {
-  static constexpr bool CTRL = G::NT >= 256;
-  static constexpr uint32_t NW = G::NT / 64, NDW = CTRL ? NW - 1 : NW;
-  static constexpr uint32_t NROW = G::SEG / 1024, K = (NROW + NDW - 1) / NDW;
-  static_assert(G::SEG % 1024 == 0, "segments are whole 1 KiB rows");
-  u32x4 e[K];
-  XYWS_DEV static bool data_wave(uint32_t wave) { return !CTRL || wave != 0; }
-  XYWS_DEV static uint32_t row(uint32_t wave, uint32_t k) { return (CTRL ? wave - 1 : wave) + NDW * k; }
-  // (a wave's row index is wave-uniform: a scalar offset, or hipcc loops over
-  // the lanes' values; rows past the segment load and store nothing)
-  XYWS_DEV static bool valid(uint32_t wave, uint32_t k) { return K * NDW == NROW || row(wave, k) < NROW; }
-  // this wave's rows of the segment at ss into registers: K loads on every
-  // path (the fill's wait then counts them)
-  // (CHK false: the caller is a data wave, so every path issues the same
-  // operations and the compiler's waits count them)
-  template <bool CHK = true>
-  XYWS_DEV void issue(const run_params& P, uint64_t ss, uint32_t tid) {
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
-    if (CHK && !data_wave(wave)) return;
-    const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss);
-#pragma unroll
-    for (uint32_t k = 0; k < K; k++) {
-      const uint32_t r = row(wave, k);
-      e[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, valid(wave, k) ? lane * 16u : OOB, r * 1024u, AUX_NT);
-    }
-  }
-  // K dropped stores (the out-of-range offset: no memory traffic) after the
-  // first loads, as the stores after every later segment's loads
-  template <bool CHK = true>
-  XYWS_DEV static void dummy(const run_params& P, uint64_t ss, uint32_t tid) {
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (CHK && !data_wave(wave)) return;
-    const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss);
-#pragma unroll
-    for (uint32_t k = 0; k < K; k++)
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rs, OOB, k * 1024u, AUX_ST);
-  }
-  template <bool CHK = true, class LT>
-  XYWS_DEV void fill(LT& L, uint32_t tid) const {
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
-    if (CHK && !data_wave(wave)) return;
-#pragma unroll
-    for (uint32_t k = 0; k < K; k++) {
-      const uint32_t r = row(wave, k);
-      if (valid(wave, k)) *reinterpret_cast<u32x4*>(&L.seg[r * 1024u + lane * 16u]) = e[k];
-    }
-  }
-};
-
-// XOR stores of a segment's rows by the data waves (sweep_io's layout): one
-// 16-byte store per chunk (skipped ones to the out-of-range offset), then the
-// chunks holding a frame boundary or a write-window edge (store_pass).
-template <class G, bool CHK = true>
-XYWS_DEV void store_rows(const run_params& P, const lds_t<G>& L, const fent* fl, const uint2* rt, uint64_t ss,
-                         uint32_t tid, uint32_t nfl, uint32_t hi_c, uint64_t wl, uint64_t whi, uint32_t wl_r,
-                         uint32_t wh_r) {
-  using IO = sweep_io<G>;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
-  if (CHK && !IO::data_wave(wave)) return;
-  const __amdgpu_buffer_rsrc_t rs = seg_rsrc<G>(P, ss);
-  uint32_t edge = 0;
-  const uint32_t put = boundary_chunks<G, IO::K>(
-      const_cast<lds_t<G>&>(L), fl, rt, nfl, 0u, hi_c, wl_r, wh_r,
-      [&](uint32_t k, uint32_t& a, uint32_t& r, bool& ok) {
-        ok = IO::valid(wave, k);
-        r = ok ? IO::row(wave, k) : 0u;
-        a = r * 1024u + lane * 16u;
-      },
-      edge);
-  u32x4 dprev = {0u, 0u, 0u, 0u};
-#pragma unroll
-  for (uint32_t k = 0; k < IO::K; k++) {
-    // (K stores on every path: a row past the segment stores nothing)
-    const bool ok = IO::valid(wave, k);
-    const uint32_t r = ok ? IO::row(wave, k) : 0u;
-    const uint32_t a = r * 1024u + lane * 16u;
-    const uint2 rw = rt[r];
-    const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
-    const uint32_t info = __builtin_amdgcn_readfirstlane(rw.x);
-    const uint32_t kw = __builtin_amdgcn_readfirstlane(rw.y);
-    u32x4 m;
-    uint32_t off;
-    if (info & ROW_FAST) {
-      m = u32x4{kw, kw, kw, kw};
-      off = lane * 16u;
-    } else if (info & ROW_SKIP) {
-      m = u32x4{0u, 0u, 0u, 0u};
-      off = OOB;
-    } else {
-      m = u32x4{0u, 0u, 0u, 0u};
-      off = ((put >> k) & 1u) ? lane * 16u : OOB;  // (boundary_chunks)
-    }
-    if (!ok) off = OOB;
-    const u32x4 d = v ^ m;
-    __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, r * 1024u, AUX_ST);
-    // (see run_chain: the store's data registers stay live past the next store)
-    asm volatile("" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
-    dprev = d;
-  }
-  asm volatile("s_nop 1" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
-#pragma nounroll
-  while (edge) {
-    const uint32_t k = __builtin_ctz(edge);
-    edge &= edge - 1;
-    const uint32_t r = IO::row(wave, k);
-    const uint32_t a = r * 1024u + lane * 16u;
-    uint32_t x = 0, y = nfl;
-    while (y - x > 1) {
-      const uint32_t mid = (x + y) >> 1;
-      if (fl[mid].start <= a) x = mid; else y = mid;
-    }
-    const u32x4 m = chunk_xor(fl, nfl, x, a);
-    if ((m.x | m.y | m.z | m.w) == 0u) continue;
-    if (a >= wl_r && a + 16 <= wh_r) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
-      __builtin_amdgcn_raw_buffer_store_b128(v ^ m, rs, lane * 16u, r * 1024u, AUX_ST);
-      asm volatile("s_nop 1" ::: "memory");
-      continue;
-    }
-    const uint64_t A = ss + a;
-#pragma nounroll
-    for (uint32_t t = 0; t < 16; t++) {
-      const uint64_t q = A + t;
-      const uint32_t mw = t < 4 ? m.x : t < 8 ? m.y : t < 12 ? m.z : m.w;
-      const uint8_t kb = (uint8_t)(mw >> (8u * (t & 3u)));
-      if (kb && q >= wl && q < whi) P.base[q] = L.seg[a + t] ^ kb;
-    }
-  }
-}
-
-// Chain-pass bookkeeping of the sweep (lane 0): no successor entry, no write
-// limit, no descriptors.
-template <class G>
-XYWS_DEV void sweep_chain_reset(lds_t<G>& L) {
-  L.known = 0; L.past = 0; L.done = 0; L.end = 0; L.ok = 0; L.tmo = 0;
-  L.hn = NONE; L.Wn = NONE; L.succ = 0; L.first_after = NONE;
-  L.cnt = 0; L.tail = 0; L.nrec = 0;
-}
-
-// The passes over the LDS segment at ss from the chain state in L.S (whole
-// workgroup; lane 0 set L.S and sweep_chain_reset): each pass chases (the dense
-// pass when the previous pass was dense, else lane 0's serial chase) and, with
-// `stores`, stores its chunks. rsv0: the first pass keeps list slot 0 for the
-// entering frame (the speculative pass). one: stop after the first pass (the
-// list stays in LDS; true when it covered the segment). Leaves L.S = the exit
-// state, L.cnt = the frames started in the segment.
-template <class G>
-XYWS_DEV bool seg_passes(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid, bool stores, bool rsv0,
-                         bool one) {
-  const uint64_t wl = P.lo, whi = P.hi;
-  const uint32_t wl_r = wl > ss ? (wl - ss < G::SEG ? (uint32_t)(wl - ss) : G::SEG) : 0u;
-  const uint32_t wh_r = whi > ss ? (whi - ss < G::SEG ? (uint32_t)(whi - ss) : G::SEG) : 0u;
-  const bool any = stores && !(P.opts & XYWS_OPT_NO_STORE) && wl_r < wh_r;
-  const bool unm = (P.opts & XYWS_OPT_UNMASKED_HINT) != 0;
-  if (rsv0 && tid == 0) L.fl[0] = fent{0u, 0u, 0u, 0u};
-  uint32_t lo_c = 0, keep = rsv0 ? 1u : 0u;
-  for (;;) {
-    __syncthreads();
-    bool dense = false;
-    if (lo_c == 0 && keep == (rsv0 ? 1u : 0u) && L.dense >= 2 * G::NSB) {
-      const cstate S0 = L.S;
-      const uint64_t se14 = ss + G::SEG + XYWS_MAX_FRAME_HEADER_SIZE;
-      constexpr uint32_t STOP = G::SEG - XYWS_MAX_FRAME_HEADER_SIZE + 1;
-      if (!(S0.st & (S_PARTIAL | S_CUT)) && S0.X >= ss && S0.X < ss + G::SB && P.hi >= se14)
-        dense = dense_pass<G>(P, L, ss, tid, unm, false, STOP, rsv0);
-    }
-    if (tid < 64) {
-      if (tid == 0 && !dense) chase_pass(P, L, ss, lo_c, keep);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (stores) build_rows<G>(L.fl, L.rt, L.nfl, lo_c, L.pass_hi, wl_r, wh_r, any, tid);
-    }
-    if (stores) {
-      if (!dense) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      store_pass<G>(P, L, ss, tid, L.nfl, lo_c, L.pass_hi, wl, whi, wl_r, wh_r);
-    } else {
-      __syncthreads();
-    }
-    const uint32_t nfl = L.nfl, hi_c = L.pass_hi;
-    if (hi_c >= G::SEG) return true;
-    if (one) return false;
-    __syncthreads();  // the list is rebuilt for the next pass
-    if (tid == 0) {   // entries reaching past hi_c (tiny frames can share its chunk) carry over
-      uint32_t c = nfl;
-      while (c > 0 && L.fl[c - 1].end > hi_c) c--;
-      for (uint32_t i = c; i < nfl; i++) L.fl[i - c] = L.fl[i];
-      L.keepn = nfl - c;
-    }
-    __syncthreads();
-    keep = L.keepn;
-    lo_c = hi_c;
-  }
-}
-
-// Stores of the single speculative pass still in LDS (whole workgroup): the
-// row table, then one store pass.
-template <class G>
-XYWS_DEV void seg_store_list(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid) {
-  const uint64_t wl = P.lo, whi = P.hi;
-  const uint32_t wl_r = wl > ss ? (wl - ss < G::SEG ? (uint32_t)(wl - ss) : G::SEG) : 0u;
-  const uint32_t wh_r = whi > ss ? (whi - ss < G::SEG ? (uint32_t)(whi - ss) : G::SEG) : 0u;
-  const bool any = !(P.opts & XYWS_OPT_NO_STORE) && wl_r < wh_r;
-  if (tid < 64) build_rows<G>(L.fl, L.rt, L.nfl, 0u, G::SEG, wl_r, wh_r, any, tid);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  store_pass<G>(P, L, ss, tid, L.nfl, 0u, G::SEG, wl, whi, wl_r, wh_r);
-}
-
-
-// Stride prediction (lane 0). In a stream of equal frames of fsz bytes through
-// a frame that ended at ref (this workgroup's last exact exit), the first frame
-// start at or after ss is the lattice point below.
-XYWS_DEV uint64_t pred_pos(uint64_t ref, uint64_t fsz, uint64_t ss) {
-  if (ref == NONE || fsz < 2) return NONE;
-  return ref >= ss ? ref : ref + (ss - ref + fsz - 1) / fsz * fsz;
-}
-
-// The 20 bytes at the dword at or below x (lane 0), for the predicted frame's
-// header before a segment: part of the next segment's prefetch group (its
-// wait is the fill's); zero past the batch.
-XYWS_DEV void cover_load(const run_params& P, uint64_t x, uint32_t r[5]) {
-  const uint64_t a = x & ~3ull;
-  const uint64_t top = (P.hi + 3) & ~3ull;
-  const uint32_t n = a < top ? (top - a < 20 ? (uint32_t)(top - a) : 20u) : 0u;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(P.base + a, 0, n, 0x00020000);
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, 0u, 0u, AUX_NT);
-  r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
-  r[4] = __builtin_amdgcn_raw_buffer_load_b32(rs, 16u, 0u, AUX_NT);
-}
-
-// The predicted entering state of the segment at ss (lane 0): the frame start
-// p = L.sw_pcur, whose header (in LDS) and whose predecessor's header (p -
-// fsz, loaded with the segment) both open frames of exactly fsz bytes a client
-// stream plausibly holds. That predecessor frame covers the segment's first
-// bytes. Speculation only: the workgroup checks it against the published exit
-// of the segment before (sweep_validate).
-template <class G>
-XYWS_DEV bool sweep_predicted(const run_params& P, const lds_t<G>& L, uint64_t ss, bool unm, const uint32_t cr[5],
-                              cstate& U) {
-  const uint64_t p = L.sw_pcur, fsz = L.sw_fcur;
-  if (p == NONE || p < ss || p >= ss + G::SEG || p >= P.hi || p < P.lo + fsz) return false;
-  const hdr_info h = hdr_at(P, L, ss, p, NONE);
-  if (!plausible(h, unm) || (uint64_t)h.hlen + h.plen != fsz) return false;
-  const uint64_t c = p - fsz;
-  const uint32_t sh = (uint32_t)(c & 3);
-  uint32_t w[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) w[i] = __builtin_amdgcn_alignbyte(cr[i + 1], cr[i], sh);
-  const hdr_info hc = parse_header_words(w, 16u);
-  if (!plausible(hc, unm) || (uint64_t)hc.hlen + hc.plen != fsz) return false;
-  U.X = p;
-  U.cov_start = c;
-  U.cov_ps = c + hc.hlen;
-  U.cov_key = hc.key;
-  U.cov_kw = aligned_key(hc.key, U.cov_ps, 0);
-  U.st = 0;
-  U.pad = 0;
-  return true;
-}
-
-// Deferred check of a predicted segment (wave 0): its assumed entering state
-// against the published exit of the segment before it (by now long published);
-// a mismatch sends the call through the finisher's repair walk.
-XYWS_DEV void sweep_validate(const run_params& P, uint64_t s, uint64_t ss, uint64_t E, uint32_t lane,
-                             const cstate& U) {
-  cstate Ein;
-  const bool ok = sweep_lookback(P, s, ss, E, lane, Ein);
-  if (lane == 0 && (!ok || !same_state(Ein, U))) {
-    __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(P.head) + HW_BAD, 1ull, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    stat_add(P, ST_BAD, 1);
-    stat_add(P, ST_SW_NOTHING, 1);
-  }
-}
-
-enum { SWM_SPEC = 0, SWM_EXACT = 1, SWM_PRED = 2, SWM_EXACT0 = 3 };
-
-// The slow path of segment s (whole workgroup). Returns the action taken (SW_*).
-template <class G>
-XYWS_DEV uint32_t sweep_slow(const run_params& P, lds_t<G>& L, uint32_t tid, uint64_t s) {
-  const uint64_t ss = s * G::SEG;
-  const uint64_t E = L.E;
-  const bool unm = (P.opts & XYWS_OPT_UNMASKED_HINT) != 0;
-  const uint32_t mode = L.sw_act;
-  uint32_t act = SW_REUSE;
-  if (mode == SWM_EXACT0 || mode == SWM_PRED) {
-    // C1. known entering state, the dense pass or several passes
-    if (tid == 0) {
-      sweep_chain_reset(L);
-      L.S = L.sw_in;
-      L.cnt = L.aux2;
-    }
-    const bool nothing = (L.sw_in.st & S_PARTIAL) != 0;
-    bool single = false;
-    if (!nothing) {
-      single = seg_passes<G>(P, L, ss, tid, false, false, true);
-      if (!single) seg_passes<G>(P, L, ss, tid, false, false, false);
-    }
-    if (tid == 0) {
-      L.sw_spec = L.S;
-      L.sw_cnt_spec = (uint32_t)L.cnt;
-      sweep_publish(P, s, E, true, L.S);
-    }
-    act = nothing ? SW_NOTHING : (single ? SW_REUSE : SW_APPLY);
-  } else {
-    // C2. unknown entering state: the quick scan
-    if ((P.opts & XYWS_OPT_TEST_SPEC) && s % 3 == 1) {
-      if (tid == 0) L.best = 0xFFFFFFFFu;  // (tests: pretend no start was found: exact mode)
-    } else {
-      sweep_scan<G>(P, L, ss, tid, unm, (P.opts & XYWS_OPT_SW_FULLSCAN) ? G::CH : 1u);
-    }
-    if (tid == 0) {
-      uint32_t b = L.best;
-      // (tests: a wrong entry one byte late)
-      if ((P.opts & XYWS_OPT_TEST_SPEC) && s % 3 == 2 && b != 0xFFFFFFFFu && ss + b + 1 < P.hi) b++;
-      const uint64_t h = b == 0xFFFFFFFFu ? NONE : ss + b;
-      L.sw_h = h;
-      sweep_chain_reset(L);
-      cstate S0;
-      S0.X = h; S0.cov_ps = h; S0.cov_start = h; S0.cov_kw = 0; S0.cov_key = 0; S0.st = S_NOCOV; S0.pad = 0;
-      L.S = S0;
-      L.sw_act = h == NONE ? SWM_EXACT : SWM_SPEC;
-      if (h != NONE) {  // dense-pass hint: the entry's frame is small
-        const hdr_info h0 = hdr_at(P, L, ss, h, NONE);
-        if (h0.hlen && h0.plen + h0.hlen < 1024) L.dense = G::FCAP;
-      }
-    }
-    __syncthreads();
-    const bool spec = L.sw_act == SWM_SPEC;
-    bool ok = true;
-    // exact mode: the entering state first
-    if (!spec) {
-      if (tid < 64) {
-        cstate Ein;
-        ok = sweep_lookback(P, s, ss, E, tid, Ein);
-        if (tid == 0) {
-          L.sw_in = Ein;
-          if (ok && !(Ein.st & S_PARTIAL)) L.S = Ein;
-          L.sw_single = ok ? 1u : 0u;
-        }
-      }
-      __syncthreads();
-      ok = L.sw_single != 0;
-    }
-    const bool nothing = !ok || (!spec && (L.sw_in.st & S_PARTIAL));
-    // the chase (no stores yet) and its publication: at once in spec mode
-    bool single = false;
-    if (!nothing) {
-      single = seg_passes<G>(P, L, ss, tid, false, spec, true);
-      if (!single) seg_passes<G>(P, L, ss, tid, false, false, false);
-    }
-    if (tid == 0) {
-      if (nothing) L.S = L.sw_in;
-      L.sw_spec = L.S;
-      L.sw_cnt_spec = (uint32_t)L.cnt;
-      sweep_publish(P, s, E, true, L.S);
-    }
-    act = nothing ? SW_NOTHING : (single ? SW_REUSE : SW_APPLY);
-    // spec mode: the entering state now; keep the list when it lands on the
-    // entry, else re-chase from it
-    if (spec) {
-      if (tid < 64) {
-        cstate Ein;
-        const bool lok = sweep_lookback(P, s, ss, E, tid, Ein);
-        if (tid == 0) {
-          uint32_t a;
-          if (!lok) a = SW_NOTHING;
-          else if (Ein.st & S_PARTIAL) a = SW_NOTHING;
-          else if (single && Ein.X == L.sw_h) a = SW_REUSE;
-          else a = SW_APPLY;
-          L.sw_in = Ein;
-          L.sw_act = a;
-          if (a == SW_REUSE) {
-            fent e = {0u, 0u, 0u, 0u};
-            if (!(Ein.st & (S_NOCOV | S_PARTCARRY)) && Ein.X > ss) {
-              e.ps = clamp_rel(Ein.cov_ps, ss);
-              e.end = clamp_rel(Ein.X, ss);
-              e.kw = Ein.cov_kw;
-            }
-            L.fl[0] = e;
-          }
-        }
-      }
-      __syncthreads();
-      act = L.sw_act;
-    }
-  }
-  if (act == SW_APPLY) {
-    if (tid == 0) {
-      sweep_chain_reset(L);
-      L.S = L.sw_in;
-      L.cnt = L.aux2;
-    }
-    seg_passes<G>(P, L, ss, tid, true, false, false);
-  }
-  return act;
-}
-
-// Decode segment s (whole workgroup; its bytes and pad in LDS). Returns the
-// frames it counts (lane 0). The entering state is
-//  * EXACT0: segment 0 — the batch start and the incoming carry;
-//  * PRED: the stride prediction held (sweep_predicted): decode at once, no
-//    waiting; the assumption is checked one segment later (sweep_validate);
-//  * otherwise the quick scan's entry (SPEC: chase, publish, look back, keep
-//    the list when the entering state lands on the entry, else re-chase), or
-//    none (EXACT: look back first, then chase).
-// Every segment publishes its exit; a segment whose final exit differs from
-// its publication counts in HW_BAD (the finisher's repair walk).
-// ROLE: the waves running this copy. With a control wave (sweep_io::CTRL) the
-// kernel runs two loops, one per role, with the same barriers: the control
-// wave's state (64-bit chain states, look-back) and the data waves' prefetch
-// registers then never share a register allocation region (one loop holding
-// both spilled the prefetch and waited for every load at each store).
-enum { SWR_ALL = 0, SWR_CTRL = 1, SWR_DATA = 2 };
-template <class G, int ROLE>
-XYWS_DEV uint64_t sweep_segment(const run_params& P, lds_t<G>& L, uint32_t tid, uint64_t s, sweep_io<G>& io,
-                                const uint32_t cr[5], uint32_t& claimed, uint64_t nx) {
-  constexpr bool CT = ROLE != SWR_DATA, DT = ROLE != SWR_CTRL;
-  const uint64_t ss = s * G::SEG;
-  const uint64_t E = L.E;
-  const bool unm = (P.opts & XYWS_OPT_UNMASKED_HINT) != 0;
-  const bool st_on = stats_on(P) && tid == 0;
-  uint64_t tq = st_on ? __builtin_amdgcn_s_memtime() : 0;
-  uint64_t* rec = P.srec + s * SR_WORDS;
-  // A. wave 0 before its own share of the next segment's loads (the other
-  //    waves issue theirs at once): the entering state, and when it is known
-  //    (EXACT0, PRED) and one lane-0 chase covers the segment, the chase and
-  //    its publication (FAST). The dense pass, the quick scan, the SPEC and
-  //    EXACT modes and several passes are the slow path below, after every
-  //    wave's loads are out.
-  if (CT && tid == 0) {
-    // this segment's first bytes for the segment before it (sweep_pad)
-    sweep_orig_publish(P, s, E, *reinterpret_cast<const u32x4*>(L.seg));
-    sweep_chain_reset(L);
-    L.aux2 = 0;
-    L.sw_h = NONE;
-    uint32_t mode = SWM_EXACT;
-    if (s == 0) {
-      // the incoming carry (the caller's, or none: zero), snapshot for the
-      // finisher (the caller's carry may alias the carry out)
-      const xyws_carry* cz = P.cin_user ? P.cin_user : &k_zero_carry;
-      uint64_t cw[8];
-#pragma unroll
-      for (int i = 0; i < 8; i++) cw[i] = reinterpret_cast<const uint64_t*>(cz)[i];
-#pragma unroll
-      for (int i = 0; i < 8; i++) st_store(reinterpret_cast<uint64_t*>(P.cin) + i, cw[i]);
-      uint64_t c0;
-      L.sw_in = initial_state(P, cz, c0);
-      L.cnt = c0;
-      L.aux2 = c0;  // (the carried-header frame, counted again when the segment is re-chased)
-      mode = SWM_EXACT0;
-    } else if (!(P.opts & XYWS_OPT_TEST_SPEC)) {
-      cstate U;
-      if (sweep_predicted<G>(P, L, ss, unm, cr, U)) {
-        L.sw_in = U;
-        L.sw_h = U.X;
-        mode = SWM_PRED;
-      }
-    }
-    L.sw_act = mode;
-    if (st_on) L.sw_t[8] += __builtin_amdgcn_s_memtime() - tq;
-    uint32_t fast = 0;
-    if ((mode == SWM_EXACT0 || mode == SWM_PRED) && !(L.sw_in.st & S_PARTIAL) && L.dense < 2 * G::NSB) {
-      L.S = L.sw_in;
-      chase_pass(P, L, ss, 0u, 0u);
-      if (L.pass_hi >= G::SEG) {
-        fast = 1;
-        L.sw_spec = L.S;
-        L.sw_cnt_spec = (uint32_t)L.cnt;
-        sweep_publish(P, s, E, true, L.S);
-      }
-    }
-    L.sw_fast = fast;
-    if (st_on) L.sw_t[1] += __builtin_amdgcn_s_memtime() - tq;
-  }
-  // the next segment's loads (wave 0 after its work above; lane 0's claim and
-  // header loads first, so that the data loads are the youngest and the fill
-  // waits for them while this segment's stores still drain)
-  if (nx < P.nseg) {
-    if (CT && tid == 0) {
-      // the claim of the segment after the next one: a returning atomic whose
-      // value is read only when the next segment's loads have been waited
-      // for (inline asm: the compiler's atomic optimizer would wait for it,
-      // and for this segment's stores, at once)
-      asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(claimed) : "v"(P.head), "v"(1u) : "memory");
-    }
-    if constexpr (DT) io.template issue<ROLE == SWR_ALL>(P, nx * G::SEG, tid);
-  }
-  const uint64_t tb0 = swt_now(P);
-  // B. fast: wave 0 builds the row table while the other waves' loads fly,
-  //    then checks the previous predicted segment
-  if (CT && tid < 64) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (L.sw_fast) {
-      const uint64_t wl = P.lo, whi = P.hi;
-      const uint32_t wl_r = wl > ss ? (wl - ss < G::SEG ? (uint32_t)(wl - ss) : G::SEG) : 0u;
-      const uint32_t wh_r = whi > ss ? (whi - ss < G::SEG ? (uint32_t)(whi - ss) : G::SEG) : 0u;
-      const bool any = !(P.opts & XYWS_OPT_NO_STORE) && wl_r < wh_r;
-      build_rows<G>(L.fl, L.rt, L.nfl, 0u, G::SEG, wl_r, wh_r, any, tid);
-    }
-    if (tid == 0 && stats_on(P)) L.sw_t[2] += __builtin_amdgcn_s_memtime() - tb0;
-  }
-  __syncthreads();
-  if (tid == 64 && stats_on(P)) L.sw_t[3] += __builtin_amdgcn_s_memtime() - tb0;
-  if (st_on) {
-    const uint64_t t = __builtin_amdgcn_s_memtime();
-    stat_add(P, ST_SW_TSCAN, t - tq);
-    tq = t;
-  }
-  const bool fast = L.sw_fast != 0;
-  const uint32_t mode = L.sw_act;
-  uint32_t act = SW_REUSE;
-  if (!fast) {
-    act = sweep_slow<G>(P, L, tid, s);
-    __syncthreads();  // (a re-chase's stores read the row table)
-  }
-  // D. the stores, on every path (one store per chunk per lane, skipped ones
-  //    to the out-of-range offset: the compiler then counts CH stores after
-  //    the next segment's loads on every path, and the next fill waits for
-  //    those loads only): the list in LDS when the segment decodes with it,
-  //    else a table of skipped rows (re-chased segments stored already)
-  {
-    const uint64_t wl = P.lo, whi = P.hi;
-    const uint32_t wl_r = wl > ss ? (wl - ss < G::SEG ? (uint32_t)(wl - ss) : G::SEG) : 0u;
-    const uint32_t wh_r = whi > ss ? (whi - ss < G::SEG ? (uint32_t)(whi - ss) : G::SEG) : 0u;
-    if (CT && tid < 64) {
-      if (act != SW_REUSE) {
-        for (uint32_t r = tid; r < G::SEG / 1024; r += 64) L.rt[r] = uint2{ROW_SKIP, 0u};
-      } else if (!fast) {
-        const bool any = !(P.opts & XYWS_OPT_NO_STORE) && wl_r < wh_r;
-        build_rows<G>(L.fl, L.rt, L.nfl, 0u, G::SEG, wl_r, wh_r, any, tid);
-      }
-    }
-    const uint64_t tl0 = swt_now(P);
-    // (XYWS_OPT_SW_LOADWAIT, an experiment: the next segment's loads land
-    // before this segment's stores issue)
-    if (DT && (P.opts & XYWS_OPT_SW_LOADWAIT)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (tid == 64 && stats_on(P)) L.sw_t[4] += __builtin_amdgcn_s_memtime() - tl0;
-    __syncthreads();
-    const uint64_t ts0 = swt_now(P);
-    if constexpr (DT) {
-      store_rows<G, ROLE == SWR_ALL>(P, L, L.fl, L.rt, ss, tid,
-                                     act == SW_REUSE ? L.nfl : 0u, act == SW_REUSE ? G::SEG : 0u, wl, whi,
-                                     wl_r, wh_r);
-    }
-    if (tid == 64 && stats_on(P)) L.sw_t[5] += __builtin_amdgcn_s_memtime() - ts0;
-    // the control wave checks the previous predicted segment while the data
-    // waves store (its look-back waits for memory: off the stores' path)
-    if (CT && tid < 64) {
-      const uint64_t vs = L.sw_vs;
-      if (vs != NONE && !(P.opts & XYWS_OPT_SWX_NOVAL)) {
-        sweep_validate(P, vs, vs * G::SEG, E, tid, L.sw_vU);
-        if (tid == 0) L.sw_vs = NONE;
-      }
-      // the next segment's list from the headers loaded in B
-    }
-  }
-  __syncthreads();
-  uint64_t cnt = 0;
-  if (CT && tid == 0) {
-    cstate F;
-    if (act == SW_REUSE) { F = L.sw_spec; cnt = L.sw_cnt_spec; }
-    else if (act == SW_APPLY) { F = L.S; cnt = L.cnt; }
-    else { F = L.sw_in; cnt = 0; }
-    const bool changed = !same_state(F, L.sw_spec);
-    if (!(P.opts & XYWS_OPT_SWX_NOREC)) {
-      put_state(rec + SR_U, L.sw_in);
-      put_state(rec + SR_F, F);
-      st_store(rec + SR_H, L.sw_h);
-      st_store(rec + SR_CNT, cnt);
-    }
-    if (changed) {
-      __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(P.head) + HW_BAD, 1ull, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      stat_add(P, ST_BAD, 1);
-    }
-    if (mode == SWM_PRED) {  // checked one segment later
-      L.sw_vs = s;
-      L.sw_vU = L.sw_in;
-    }
-    // the stride reference for the following predictions
-    const uint64_t fs = F.X - F.cov_start;
-    const bool ref = !(F.st & (S_NOCOV | S_PARTIAL | S_PARTCARRY | S_CARRIED | S_HDRCARRY)) && F.X < P.hi &&
-                     F.X > F.cov_start && fs <= XCLAMP;
-    L.sw_ref = ref ? F.X : NONE;
-    L.sw_fsz = ref ? fs : 0;
-    if (cnt) {  // (the decoder choice: the workgroup's range of last-frame sizes)
-      const uint64_t lf = last_frame_size(F);
-      if (lf) {
-        if (lf > L.sw_fsmax) L.sw_fsmax = lf;
-        if (lf < L.sw_fsmin) L.sw_fsmin = lf;
-      }
-    }
-    if (act == SW_APPLY) stat_add(P, ST_SW_APPLY, 1);
-    if (!fast) stat_add(P, ST_SW_DEFER, 1);
-    if (mode != SWM_PRED && mode != SWM_EXACT0) stat_add(P, ST_SW_WIN, 1);
-    stat_add(P, ST_SEGS, 1);
-    if (st_on) stat_add(P, ST_T_XOR, __builtin_amdgcn_s_memtime() - tq);
-  }
-  return cnt;
-}
-
-// Redo segment s from the exact entering state Ex after undoing what it did
-// from U (whole workgroup; the finisher); its pad is the next segment's
-// recorded original bytes. Leaves L.S = the new exit, L.cnt = its frames
-// (counting the carried-header frame for segment 0: c0).
-template <class G>
-XYWS_DEV void sweep_redo(const run_params& P, lds_t<G>& L, uint32_t tid, uint64_t s, const cstate& U,
-                         const cstate& Ex, uint64_t c0) {
-  const uint64_t ss = s * G::SEG;
-  seg_io<G> io;
-  for (int pass = 0; pass < 2; pass++) {
-    __syncthreads();
-    io.fill(P, L, ss, tid);
-    if (tid == 0) {
-      sweep_pad<G>(P, L, ss);  // (published long ago)
-      sweep_chain_reset(L);
-      L.S = pass == 0 ? U : Ex;
-      L.cnt = pass == 0 ? 0 : c0;
-      L.dense = 0;
-    }
-    __syncthreads();
-    const cstate S0 = L.S;
-    // (a segment that stored nothing: its entering state ended the batch in a header)
-    if (!(S0.st & S_PARTIAL)) seg_passes<G>(P, L, ss, tid, true, false, false);
-    // the stores land before the next pass reloads the segment
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-}
-
-// The first segment k >= from whose recorded entering state differs from the
-// recorded final exit of k-1 (whole workgroup, 1024 segments at a time), nseg
-// if none.
-template <class G>
-XYWS_DEV uint64_t sweep_next_bad(const run_params& P, lds_t<G>& L, uint32_t tid, uint64_t from) {
-  for (uint64_t k0 = from; k0 < P.nseg; k0 += G::NT) {
-    if (tid == 0) L.aux0 = NONE;
-    __syncthreads();
-    const uint64_t k = k0 + tid;
-    if (k < P.nseg && k > 0) {
-      const cstate U = get_state(P.srec + k * SR_WORDS + SR_U);
-      const cstate F = get_state(P.srec + (k - 1) * SR_WORDS + SR_F);
-      if (!same_state(U, F)) atomicMin(reinterpret_cast<unsigned long long*>(&L.aux0), (unsigned long long)k);
-    }
-    __syncthreads();
-    const uint64_t f = L.aux0;
-    __syncthreads();
-    if (f != NONE) return f;
-  }
-  return P.nseg;
-}
-
-// Repair walk (whole workgroup; the finisher, when a segment's final exit
-// differs from the one it published): every segment whose recorded entering
-// state is not the final exit of the segment before it is undone and redone
-// from that exit, in order, until none is left. Segment 0's entering state is
-// exact (the batch start and the carry); by induction every segment is then
-// exact. Returns the change of the frame total.
-template <class G>
-XYWS_DEV int64_t sweep_repair(const run_params& P, lds_t<G>& L, uint32_t tid) {
-  int64_t dtot = 0;
-  if (tid == 0) L.sw_next = NONE;  // (every segment's first bytes are published: sweep_pad)
-  uint64_t k = sweep_next_bad<G>(P, L, tid, 1);
-  while (k < P.nseg) {
-    uint64_t* rk = P.srec + k * SR_WORDS;
-    if (tid == 0) {
-      L.B = get_state(P.srec + (k - 1) * SR_WORDS + SR_F);
-      L.sw_spec = get_state(rk + SR_U);
-      L.sw_cnt_spec = (uint32_t)st_load(rk + SR_CNT);
-    }
-    __syncthreads();
-    const cstate U = L.sw_spec, Ex = L.B;
-    sweep_redo<G>(P, L, tid, k, U, Ex, 0);
-    if (tid == 0) {
-      dtot += (int64_t)L.cnt - (int64_t)L.sw_cnt_spec;
-      put_state(rk + SR_U, Ex);
-      put_state(rk + SR_F, L.S);
-      st_store(rk + SR_CNT, L.cnt);
-      stat_add(P, ST_REPAIR, 1);
-    }
-    __syncthreads();
-    k = sweep_next_bad<G>(P, L, tid, k + 1);
-  }
-  return dtot;
-}
-
-// The workgroup whose done-count add came last (every other has exited and
-// released its stores): the repair walk when a segment's final exit differs
-// from its publication, then the call's outputs from the last segment's final
-// exit; resets the end-of-call words and the claim counter and advances the
-// epoch.
-template <class G>
-XYWS_DEV void sweep_finish(const run_params& P, lds_t<G>& L, uint32_t tid) {
-  uint64_t* hw = reinterpret_cast<uint64_t*>(P.head);
-  if (tid == 0) L.aux1 = st_load(hw + HW_BAD);
-  __syncthreads();
-  int64_t dtot = 0;
-  if (L.aux1) dtot = sweep_repair<G>(P, L, tid);
-  if (tid == 0) {
-    uint64_t c[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) c[i] = st_load(reinterpret_cast<const uint64_t*>(P.cin) + i);
-    const uint64_t total = st_load(hw + HW_TOTAL) + (uint64_t)dtot;
-    const cstate S = get_state(P.srec + (P.nseg - 1) * SR_WORDS + SR_F);
-#pragma unroll
-    for (int i = 0; i < 8; i++) reinterpret_cast<uint64_t*>(&L.cinc)[i] = c[i];
-    write_outputs(P, &L.cinc, total, S);
-    pol_publish(P, L.E, 1);
-    st_store(hw + HW_BAD, 0);
-    st_store(hw + HW_TOTAL, 0);
-    st_store(hw + HW_DONE, 0);
-    __hip_atomic_store(P.head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    st_store(reinterpret_cast<uint64_t*>(P.head + HEAD_EPOCH), L.E);
-  }
-}
-
-// The segment loop of one role (sweep_segment): the data waves prefetch the
-// next segment into registers and fill LDS from them; the control wave takes
-// the claims. Returns lane 0's frame count.
-template <class G, int ROLE>
-XYWS_DEV uint64_t sweep_loop(const run_params& P, lds_t<G>& L, uint32_t tid0, uint32_t& claimed) {
-  constexpr bool CT = ROLE != SWR_DATA, DT = ROLE != SWR_CTRL;
-  uint32_t tid = tid0;
-  asm volatile("" : "+v"(tid));
-  sweep_io<G> io;
-  // lane 0: the predicted predecessor header of this segment and of the next
-  // (sweep_predicted)
-  uint32_t cr[5] = {0u, 0u, 0u, 0u, 0u}, crn[5] = {0u, 0u, 0u, 0u, 0u};
-  uint64_t frames = 0;                     // lane 0
-  uint64_t cur = uniform64(L.sw_cur);
-  if (DT && cur < P.nseg) {
-    io.template issue<ROLE == SWR_ALL>(P, cur * G::SEG, tid);
-    sweep_io<G>::template dummy<ROLE == SWR_ALL>(P, cur * G::SEG, tid);  // (as after every segment: stores younger than the loads)
-  }
-  while (cur < P.nseg) {
-    // (the lane index made opaque per segment: hipcc would otherwise hoist the
-    // lanes' address math out of this loop and spill it)
-    asm volatile("" : "+v"(tid));
-    const uint64_t ti0 = swt_now(P);
-    __syncthreads();  // the previous segment's LDS reads are done
-    if constexpr (DT) io.template fill<ROLE == SWR_ALL>(L, tid);
-    if (tid == 64 && stats_on(P)) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      L.sw_t[6] += __builtin_amdgcn_s_memtime() - ti0;
-    }
-    if (CT && tid == 0) {
-      const uint64_t tc0 = swt_now(P);
-      // the bytes after the segment: unknown (stale in LDS; the speculation
-      // may read them) until a header straddles its end (sweep_pad)
-      L.sw_padok = 0;
-      // the segment claimed during the previous segment (lane 0's atomic:
-      // wave 0 waits for its own few memory operations)
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(claimed)::"memory");
-      const uint64_t nx = claimed < P.nseg ? claimed : NONE;
-      L.sw_next = nx;
-      // the stride prediction for the next segment, and its predecessor's
-      // header: loaded before the data waves issue the next segment's bytes,
-      // so that they return ahead of them
-      L.sw_pcur = L.sw_pnx;  // (this segment's, made one segment ago)
-      L.sw_fcur = L.sw_fnx;
-      L.sw_pnx = NONE;
-      if (nx < P.nseg) {
-        const uint64_t pn = pred_pos(L.sw_ref, L.sw_fsz, nx * G::SEG);
-        L.sw_pnx = pn;
-        L.sw_fnx = L.sw_fsz;
-        if (pn != NONE && pn >= L.sw_fsz) cover_load(P, pn - L.sw_fsz, crn);
-      }
-      if (stats_on(P)) L.sw_t[0] += __builtin_amdgcn_s_memtime() - tc0;
-    }
-    __syncthreads();
-    const uint64_t nx = uniform64(L.sw_next);
-    frames += sweep_segment<G, ROLE>(P, L, tid, cur, io, cr, claimed, nx);
-#pragma unroll
-    for (int i = 0; i < 5; i++) cr[i] = crn[i];
-    if (tid == 64 && stats_on(P)) L.sw_t[7] += __builtin_amdgcn_s_memtime() - ti0;
-    cur = nx;
-  }
-  // the last predicted segment's check
-  if (CT && tid < 64 && L.sw_vs != NONE) sweep_validate(P, L.sw_vs, L.sw_vs * G::SEG, L.E, tid, L.sw_vU);
-  return frames;
-}
-
-template <class G>
-__global__ void __launch_bounds__(G::NT, G::WPE) k_stream_sweep(run_params P) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
-  lds_t<G>& L = *reinterpret_cast<lds_t<G>*>(xs_lds);
-  const uint32_t tid0 = threadIdx.x;
-  uint32_t claimed = 0;  // lane 0: the segment claimed one iteration ahead (its atomic's value is used later)
-  if (tid0 == 0) {
-    L.E = st_load(reinterpret_cast<const uint64_t*>(P.head + HEAD_EPOCH)) + 1;
-    const uint64_t c = atomicAdd(P.head, 1u);
-    L.sw_cur = c;
-    if (c < P.nseg) claimed = atomicAdd(P.head, 1u);
-    else claimed = 0xFFFFFFFFu;
-    L.dense = 0;
-    L.sw_ref = NONE;
-    L.sw_fsz = 0;
-    L.sw_pcur = NONE;
-    L.sw_fcur = 0;
-    L.sw_pnx = NONE;
-    L.sw_fnx = 0;
-    L.sw_vs = NONE;
-    L.sw_fsmin = ~0ull;
-    L.sw_fsmax = 0;
-#pragma unroll
-    for (int i = 0; i < 9; i++) L.sw_t[i] = 0;
-  }
-  __syncthreads();
-  uint64_t frames = 0;  // lane 0
-  if constexpr (sweep_io<G>::CTRL) {
-    // (a wave-uniform branch the compiler sees as one: each loop is a scalar
-    // branch target, never an exec-masked region whose barriers another
-    // wave would not meet)
-    if (__builtin_amdgcn_readfirstlane(tid0 >> 6) == 0) frames = sweep_loop<G, SWR_CTRL>(P, L, tid0, claimed);
-    else (void)sweep_loop<G, SWR_DATA>(P, L, tid0, claimed);
-  } else {
-    frames = sweep_loop<G, SWR_ALL>(P, L, tid0, claimed);
-  }
-  if (stats_on(P)) {
-    __syncthreads();
-    if (tid0 == 0) {
-      const uint32_t slot[8] = {ST_SWT_CLAIMW, ST_SWT_A, ST_SWT_B, ST_SWT_DBAR, ST_SWT_DLOAD, ST_SWT_DSTORE,
-                                ST_SWT_DFILL, ST_SWT_ITER};
-#pragma unroll
-      for (int i = 0; i < 8; i++) stat_add(P, slot[i], L.sw_t[i]);
-      stat_add(P, ST_SWT_PRED, L.sw_t[8]);
-    }
-  }
-  if (tid0 == 0 && frames)
-    __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(P.head) + HW_TOTAL, frames, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-  if (tid0 == 0) fs_note(P, L.sw_fsmin, L.sw_fsmax);
-  // end of the workgroup: the finisher may re-read any segment's stored bytes
-  // (the repair walk), so every storing wave drains, then an agent-scope
-  // release before the done-count add and an acquire in the finisher
-  // (MI355X_MICROARCH.md §Workgroup dispatch, valid forms)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid0 == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t last = atomicAdd(P.head + 2 * HW_DONE, 1u) + 1 == gridDim.x ? 1u : 0u;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    L.act = last;
-  }
-  __syncthreads();
-  if (L.act) sweep_finish<G>(P, L, tid0);
-}
-
-template <class G>
-int set_sweep_lds_attr() {
-  static std::mutex mu;
-  static bool done[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return XYWS_ERR_HIP;
-  std::lock_guard<std::mutex> lk(mu);
-  if (done[dev]) return XYWS_OK;
-  if (hipFuncSetAttribute((const void*)k_stream_sweep<G>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)sizeof(lds_t<G>)) != hipSuccess)
-    return XYWS_ERR_HIP;
-  done[dev] = true;
-  return XYWS_OK;
-}
-
 #include "xyws_lattice.h"
-
-template <class G>
-int launch_sweep(const run_params& P, uint32_t grid, hipStream_t stream) {
-  if (const int rc = set_sweep_lds_attr<G>()) return rc;
-  hipLaunchKernelGGL(k_stream_sweep<G>, dim3(grid), dim3(G::NT), sizeof(lds_t<G>), stream, P);
-  return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
-}
 
 constexpr uint64_t HEAD_BYTES = 1024;  // u32 [0] ticket, [1] error, [2..3] total, [4..5] epoch; bytes [64..128) carry,
                                        // [128..512) stats, [512..576) end-of-call words (HW_*)
@@ -4125,9 +2827,6 @@ int launch_runs(const run_params& P, hipStream_t stream) {
 }  // namespace
 
 void stream_scratch_init(stream_scratch* s, int device) {
-  s->smem = nullptr;
-  s->sbytes = 0;
-  s->max_segs = 0;
   s->mem = nullptr;
   s->bytes = 0;
   s->max_runs = 0;
@@ -4158,10 +2857,6 @@ void stream_scratch_free(stream_scratch* s) {
   if (s->pol_h) (void)hipHostFree(const_cast<uint64_t*>(s->pol_h));
   s->pol_h = nullptr;
   s->pol_d = nullptr;
-  if (s->smem) (void)hipFree(s->smem);
-  s->smem = nullptr;
-  s->sbytes = 0;
-  s->max_segs = 0;
   if (s->lmem) (void)hipFree(s->lmem);
   s->lmem = nullptr;
   s->lmax_segs = 0;
@@ -4218,29 +2913,6 @@ static int scratch_grow(stream_scratch* s, uint64_t runs) {
   s->bytes = bytes;
   s->max_runs = want;
   return xyws_internal::zero_now(m, records_off(want)) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
-}
-
-// Sweep decoder scratch for up to `segs` segments: entry granules (32 B per
-// segment) | flag bitmap | records (SR_WORDS x 8 B per segment); granules and
-// bitmap zeroed at allocation (epoch 0: stale; no flags).
-static uint64_t sweep_gran_bytes(uint64_t segs) { return (64 * segs + 255) & ~255ull; }
-static uint64_t sweep_bits_bytes(uint64_t segs) { return (((segs + 63) / 64) * 8 + 255) & ~255ull; }
-static int sweep_grow(stream_scratch* s, uint64_t segs, bool capturing) {
-  if (s->smem && segs <= s->max_segs) return XYWS_OK;
-  if (capturing) return XYWS_ERR_CAPACITY;
-  const uint64_t want = segs < 64 ? 64 : segs;
-  const uint64_t zb = sweep_gran_bytes(want) + sweep_bits_bytes(want);
-  const uint64_t bytes = zb + want * SR_WORDS * 8;
-  void* m = nullptr;
-  if (hipMalloc(&m, bytes) != hipSuccess) return XYWS_ERR_NOMEM;
-  if (s->smem) {
-    (void)hipDeviceSynchronize();
-    (void)hipFree(s->smem);
-  }
-  s->smem = m;
-  s->sbytes = bytes;
-  s->max_segs = want;
-  return xyws_internal::zero_now(m, zb) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
 
 // Lattice decoder scratch for up to `segs` segments: LW_STAT words of
@@ -4304,8 +2976,6 @@ int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
     if (n > runs) runs = n;
   }
   if (const int rc = scratch_grow(s, runs)) return rc;
-  // the sweep decoder's segments (production geometry)
-  if (const int rc = sweep_grow(s, (max_batch_bytes + 15 + G_SWEEP::SEG - 1) / G_SWEEP::SEG, false)) return rc;
   // the lattice decoder's (production geometry)
   return lat_grow(s, (max_batch_bytes + 15 + G_LAT::SEG - 1) / G_LAT::SEG, false);
 }
@@ -4333,23 +3003,6 @@ uint32_t stream_scratch_error(stream_scratch* s, bool clear) {
   return v[1];
 }
 
-// The decoder choice for a call without descriptors, from what the previous
-// call on this scratch (this stream) found (the policy words its finisher
-// wrote; read without waiting for it: a value one call old at most matters
-// for speed only). The sweep decoder (segments claimed from one counter:
-// every CU streams to the end of the batch) is faster when the frames are
-// large and regular, so that each segment's entry follows from the stride of
-// the frames before it (c3 / c5: 64 KiB frames, profiles/r03*); the run
-// decoder (one contiguous range per CU, one entry scan per run) is faster on
-// small frames (its dense pass) and on irregular ones (no stride to follow).
-// Regular: every run's or segment's last frame has the same size. Both
-// decoders are exact on any bytes.
-constexpr uint64_t SWEEP_MIN_FRAME = 16384;
-static bool sweep_preferred(const stream_scratch* s, uint64_t len) {
-  if (!s->pol_h || len < (64ull << 20)) return false;
-  const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
-  return fsmax && fsmin == fsmax && fsmin >= SWEEP_MIN_FRAME;
-}
 // The run decoder's geometry, by the same statistics: regular frames under
 // WG512_MAX_FRAME take two 512-thread workgroups per CU on 64 KiB segments
 // (while one workgroup chases its segment, the other's stores drain: c2's
@@ -4421,47 +3074,11 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
   }
   const bool small = (opts & XYWS_OPT_SMALL_SEG) != 0;
-  hipStreamCaptureStatus cs0 = hipStreamCaptureStatusNone;
-  (void)hipStreamIsCapturing(stream, &cs0);
-  const bool capt = cs0 != hipStreamCaptureStatusNone;
-  // The sweep decoder takes a call that asks for it, or that the decoder
-  // choice gives it (sweep_preferred), with no descriptors and none of the
-  // run decoder's own modes.
   constexpr uint32_t RUN_MODES = XYWS_OPT_PARSE_ONLY | XYWS_OPT_WG512 | XYWS_OPT_DIAG | XYWS_OPT_TEST_GIVEUP |
                                  XYWS_OPT_STEAL | XYWS_OPT_TEST_STEAL | XYWS_OPT_RUNS | XYWS_OPT_NO_LATTICE |
                                  XYWS_OPT_RUNS_NOWAIT | XYWS_OPT_WG1024 | XYWS_OPT_NO_LATENTRY;
-  const bool want_lat = !(opts & (RUN_MODES | XYWS_OPT_SWEEP | XYWS_OPT_NO_LATDEC | XYWS_OPT_TEST_SPEC)) &&
+  const bool want_lat = !(opts & (RUN_MODES | XYWS_OPT_NO_LATDEC)) &&
                         ((opts & XYWS_OPT_LATTICE) || (!small && lattice_preferred(s)));
-  const bool want_sweep = (opts & XYWS_OPT_SWEEP) || (!small && sweep_preferred(s, hi - lo));
-  if (!want_lat && want_sweep && !(frames && cap) && !(opts & RUN_MODES)) {
-    const uint64_t seg = small ? G_SWEEP_SMALL::SEG : G_SWEEP::SEG;
-    const uint64_t nseg = (hi + seg - 1) / seg;
-    if (!s->mem) {  // (the head words: claim counter, epoch, end-of-call words)
-      if (capt) return XYWS_ERR_CAPACITY;
-      if (const int rc = scratch_grow(s, 64)) return rc;
-    }
-    if (const int rc = sweep_grow(s, nseg, capt)) return rc;
-    uint8_t* m = static_cast<uint8_t*>(s->mem);
-    uint8_t* sm = static_cast<uint8_t*>(s->smem);
-    run_params P;
-    P.pfs = 0;
-    memset(&P, 0, sizeof(P));
-    P.base = base; P.lo = lo; P.hi = hi;
-    P.cout = cout; P.frames = nullptr; P.cap = 0; P.nframes = nframes;
-    P.head = reinterpret_cast<uint32_t*>(m);
-    P.cin_user = cin;
-    P.cin = reinterpret_cast<xyws_carry*>(m + 64);
-    P.opts = opts;
-    P.nseg = nseg;
-    P.sgran = reinterpret_cast<uint64_t*>(sm);
-    P.sbits = reinterpret_cast<uint64_t*>(sm + sweep_gran_bytes(s->max_segs));
-    P.srec = reinterpret_cast<uint64_t*>(sm + sweep_gran_bytes(s->max_segs) + sweep_bits_bytes(s->max_segs));
-    P.pol = s->pol_d;
-    if ((opts & XYWS_OPT_STATS) && hipMemsetAsync(m + 128, 0, 8 * XYWS_NSTATS, stream) != hipSuccess) return XYWS_ERR_HIP;
-    const uint64_t maxg = small ? 64 : (uint64_t)s->ncu;
-    const uint32_t grid = (uint32_t)(nseg < maxg ? nseg : maxg);
-    return small ? launch_sweep<G_SWEEP_SMALL>(P, grid, stream) : launch_sweep<G_SWEEP>(P, grid, stream);
-  }
   const bool mid = !small && !(opts & (XYWS_OPT_WG512 | XYWS_OPT_WG1024)) &&
                    ((opts & XYWS_OPT_WG256) || mid_preferred(s, hi - lo));
   const bool wg512 = !small && !mid && !(opts & XYWS_OPT_WG1024) && ((opts & XYWS_OPT_WG512) || wg512_preferred(s, hi - lo));
@@ -4511,7 +3128,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   P.segb = (uint32_t)seg;
   P.tbias = 0;
   P.obias = 0;
-  P.nseg = 0; P.sgran = nullptr; P.srec = nullptr; P.sbits = nullptr;
+  P.nseg = 0;
   // the lattice entry (find_entry): the previous call's frames all F bytes
   // long, several per segment
   P.pfs = 0;
@@ -4541,6 +3158,11 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     const uint64_t lnseg = (hi + lseg - 1) / lseg;
     if (const int rc = lat_grow(s, lnseg, cs != hipStreamCaptureStatusNone)) return rc;
     run_params PL = P;
+    // after a call the lattice decoder finished, no first-segment gate (its
+    // speculative stores are undone as any others; breaks at frames 1 and 2
+    // are caught before anything is stored)
+    PL.opts &= ~XYWS_OPT_LAT_NOGATE;
+    if (s->pol_h && s->pol_h[0] && (s->pol_h[4] & 3) == 3 && !(opts & XYWS_OPT_LAT_GATE)) PL.opts |= XYWS_OPT_LAT_NOGATE;
     PL.lat = static_cast<uint64_t*>(s->lmem);
     PL.lgrp = PL.lat + LW_STAT + s->lmax_segs;
     PL.lbrk = PL.lat + lat_rep_off(s->lmax_segs);
