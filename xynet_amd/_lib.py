@@ -28,6 +28,8 @@ OPT_TEST_STEAL = 0x800000
 OPT_RUNS = 0x80000000      # the run decoder whatever the decoder choice would take
 OPT_LATTICE = 0x400        # the lattice decoder first (the run decoder after it takes what it leaves)
 OPT_NO_LATDEC = 0x800      # never the lattice decoder
+OPT_TABLE = 0x10000000     # the table decoder (index + stream) whatever the decoder choice would take
+OPT_NO_TABLE = 0x20000000  # never the table decoder
 # debug stats indices (xyws_stream.hip)
 ST_RUNS, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRAMES = range(8)
 ST_GIVEUP, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS = 32, 33, 34, 35, 36
@@ -139,6 +141,8 @@ def load():
     L.xyws_debug_policy.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
     L.xyws_debug_records.restype = C.c_int64
     L.xyws_debug_records.argtypes = [vp, vp, C.POINTER(C.c_uint64), u64]
+    L.xyws_debug_table.restype = C.c_int64
+    L.xyws_debug_table.argtypes = [vp, vp, C.POINTER(C.c_uint64), u64]
     L.xyws_decode_stream.restype = i32
     L.xyws_decode_stream.argtypes = [vp, vp, u64, vp, vp, vp, u64, vp, u32, vp]
     L.xyws_decode_stream_iov.restype = i32

@@ -494,6 +494,18 @@ int64_t xyws_debug_records(xyws_ctx* ctx, void* stream, uint64_t* out, uint64_t 
   return XYWS_ERR_INVALID;
 }
 
+// Internal: the table decoder's control words (64 u64: coverage, first run
+// not covered, ...), run bases (1024) and run records (16 u64 per run) of the
+// last call on `stream`; returns the words copied. Synchronizes the device.
+int64_t xyws_debug_table(xyws_ctx* ctx, void* stream, uint64_t* out, uint64_t words) {
+  if (!ctx || !out) return XYWS_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  device_guard g(ctx->device);
+  for (auto& sl : ctx->slot)
+    if (sl.bound && sl.stream == (hipStream_t)stream) return stream_scratch_table(&sl.ss, out, words);
+  return XYWS_ERR_INVALID;
+}
+
 // Internal: the decoder-choice words the last fused stream decode on `stream`
 // published ({epoch, batch bytes, smallest, largest last-frame size, decoder:
 // 0 runs / 1 sweep / 2 runs in 512-thread workgroups}). Synchronizes the device.

@@ -271,6 +271,14 @@ struct run_params {
   uint64_t* lsl;   // lattice decoder: the workgroups' speculative-store lists (LAT_LSW words each)
   uint32_t segb;
   uint64_t tbias, obias;
+  // table decoder (xyws_table.h): control words, run records, segment
+  // descriptors (TD_W granules each), frame records (trcap per run),
+  // segments per run range
+  uint64_t* tctl;
+  uint64_t* trec;
+  uint4* tdesc;
+  xyws_frame* tlist;
+  uint64_t trcap, tspr;
 };
 
 // (xyws_lattice.h, included below)
@@ -2792,6 +2800,7 @@ __global__ void k_stream_empty(const xyws_carry* cin, xyws_carry* cout, uint64_t
 }
 
 #include "xyws_lattice.h"
+#include "xyws_table.h"
 
 constexpr uint64_t HEAD_BYTES = 1024;  // u32 [0] ticket, [1] error, [2..3] total, [4..5] epoch; bytes [64..128) carry,
                                        // [128..512) stats, [512..576) end-of-call words (HW_*)
@@ -2837,6 +2846,8 @@ void stream_scratch_init(stream_scratch* s, int device) {
   s->pol_d = nullptr;
   s->lmem = nullptr;
   s->lmax_segs = 0;
+  s->tmem = nullptr;
+  s->tbytes = 0;
   void* ph = nullptr;
   if (hipHostMalloc(&ph, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
     void* pd = nullptr;
@@ -2860,6 +2871,9 @@ void stream_scratch_free(stream_scratch* s) {
   if (s->lmem) (void)hipFree(s->lmem);
   s->lmem = nullptr;
   s->lmax_segs = 0;
+  if (s->tmem) (void)hipFree(s->tmem);
+  s->tmem = nullptr;
+  s->tbytes = 0;
   if (s->mem) (void)hipFree(s->mem);
   if (s->fmem) (void)hipFree(s->fmem);
   s->mem = nullptr;
@@ -2939,6 +2953,46 @@ static int lat_grow(stream_scratch* s, uint64_t segs, bool capturing) {
   return xyws_internal::zero_now(m, bytes) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
 
+// Table decoder geometry for a batch of hi bytes (from the 16-byte aligned
+// base): R run ranges of spr segments of TG::SEG bytes, trcap frame records
+// per run; false when the batch does not fit it (the run decoder then).
+struct tab_geom {
+  uint64_t nseg, spr, R, rcap;
+};
+template <class TG>
+static bool tab_geometry(const stream_scratch* s, uint64_t hi, bool small, tab_geom& g) {
+  g.nseg = (hi + TG::SEG - 1) / TG::SEG;
+  const uint64_t rmax = small ? 64 : (uint64_t)s->ncu;
+  g.spr = (g.nseg + rmax - 1) / rmax;
+  if (!g.spr) g.spr = 1;
+  g.R = (g.nseg + g.spr - 1) / g.spr;
+  const uint64_t rb = g.spr * TG::SEG;
+  g.rcap = rb / 1024 > 1024 ? rb / 1024 : 1024;
+  return g.spr <= TSPR_MAX && g.R >= 1 && g.R <= TAB_MAX_RUNS;
+}
+// Scratch: control words and per-run words (TW_WORDS, zeroed at allocation) |
+// run records | segment descriptors | frame records
+static uint64_t tab_bytes(const tab_geom& g, uint64_t* desc_off, uint64_t* list_off) {
+  const uint64_t ctl = 8 * TW_WORDS, rec = 8 * TR_WORDS * g.R;
+  const uint64_t desc = 16ull * TD_W * g.nseg;
+  *desc_off = (ctl + rec + 255) & ~255ull;
+  *list_off = (*desc_off + desc + 255) & ~255ull;
+  return *list_off + sizeof(xyws_frame) * g.R * g.rcap;
+}
+static int tab_grow(stream_scratch* s, uint64_t bytes, bool capturing) {
+  if (s->tmem && bytes <= s->tbytes) return XYWS_OK;
+  if (capturing) return XYWS_ERR_CAPACITY;
+  void* m = nullptr;
+  if (hipMalloc(&m, bytes) != hipSuccess) return XYWS_ERR_NOMEM;
+  if (s->tmem) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(s->tmem);
+  }
+  s->tmem = m;
+  s->tbytes = bytes;
+  return xyws_internal::zero_now(m, 8 * TW_WORDS) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
+}
+
 int stream_scratch_unmask_counter(stream_scratch* s, bool capturing, uint32_t** out) {
   if (const int rc = lat_grow(s, 1, capturing)) return rc;
   *out = reinterpret_cast<uint32_t*>(static_cast<uint64_t*>(s->lmem) + LW_UNMASK);
@@ -2976,6 +3030,12 @@ int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
     if (n > runs) runs = n;
   }
   if (const int rc = scratch_grow(s, runs)) return rc;
+  // the table decoder's (production geometry)
+  tab_geom tg;
+  if (tab_geometry<G_TAB>(s, max_batch_bytes + 15, false, tg)) {
+    uint64_t d, l;
+    if (const int rc = tab_grow(s, tab_bytes(tg, &d, &l), false)) return rc;
+  }
   // the lattice decoder's (production geometry)
   return lat_grow(s, (max_batch_bytes + 15 + G_LAT::SEG - 1) / G_LAT::SEG, false);
 }
@@ -2985,6 +3045,17 @@ int stream_scratch_stats(stream_scratch* s, uint64_t out[XYWS_NSTATS]) {
   if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
   return hipMemcpy(out, static_cast<uint8_t*>(s->mem) + 128, 8 * XYWS_NSTATS, hipMemcpyDeviceToHost) == hipSuccess
              ? XYWS_OK : XYWS_ERR_HIP;
+}
+
+// The table decoder's control words (64) and run records (TR_WORDS each), as
+// many words as fit `words`; returns the count copied. Synchronizes the device.
+int64_t stream_scratch_table(stream_scratch* s, uint64_t* out, uint64_t words) {
+  if (!s->tmem) return XYWS_ERR_INVALID;
+  if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
+  const uint64_t most = TW_WORDS + TAB_MAX_RUNS * TR_WORDS;
+  const uint64_t avail = s->tbytes / 8 < most ? s->tbytes / 8 : most;
+  const uint64_t n = words < avail ? words : avail;
+  return hipMemcpy(out, s->tmem, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int64_t)n : XYWS_ERR_HIP;
 }
 
 int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_recs) {
@@ -3039,6 +3110,21 @@ static bool wg512_preferred(const stream_scratch* s, uint64_t len) {
 // stream (XYWS_OPT_REDIRECT) and decodes what it left: nothing (it exits at
 // once), the batch from the first frame off the lattice, or all of it. Its
 // miss costs its loads of the batch's first segments.
+// The table decoder (xyws_table.h) would take a batch of at least
+// TAB_MIN_BATCH bytes after a call whose frames had mixed sizes, some of them
+// large (the largest last frame at least TAB_MIN_FRAME: config 4's 1 B - 1 MiB
+// frames). Measured slower than the run decoder on c4 (0.57 vs 0.51 ms: its
+// stream kernel takes 0.345 ms, at the lattice decoder's rate, but the index
+// kernel 0.22 ms, latency-bound on the entry scans and the header chases,
+// DESIGN §4.5), so it is opt-in (XYWS_OPT_TABLE) until the index is hidden.
+constexpr bool TAB_AUTO = false;
+constexpr uint64_t TAB_MIN_FRAME = 16384, TAB_MIN_BATCH = 64ull << 20;
+static bool table_preferred(const stream_scratch* s, uint64_t len) {
+  if (!TAB_AUTO || !s->pol_h || !s->pol_h[0] || len < TAB_MIN_BATCH) return false;
+  const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
+  return fsmax && fsmin != fsmax && fsmax >= TAB_MIN_FRAME;
+}
+
 static bool lattice_preferred(const stream_scratch* s) {
   if (!s->pol_h) return false;
   const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
@@ -3065,6 +3151,30 @@ int launch_lattice(const run_params& P, uint32_t grid, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
 
+template <class G, class TG>
+int launch_table(const run_params& P, const tab_geom& g, uint64_t gcap, hipStream_t stream) {
+  static std::mutex mu;
+  static bool done[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return XYWS_ERR_HIP;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!done[dev]) {
+      if (hipFuncSetAttribute((const void*)k_stream_index<G, TG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sizeof(idx_lds<G>)) != hipSuccess ||
+          hipFuncSetAttribute((const void*)k_stream_table<TG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sizeof(tab_lds<TG>)) != hipSuccess)
+        return XYWS_ERR_HIP;
+      done[dev] = true;
+    }
+  }
+  hipLaunchKernelGGL((k_stream_index<G, TG>), dim3((uint32_t)g.R), dim3(G::NT), sizeof(idx_lds<G>), stream, P);
+  const uint64_t grid = g.nseg < gcap ? g.nseg : gcap;
+  hipLaunchKernelGGL(k_stream_table<TG>, dim3((uint32_t)grid), dim3(TG::NT), sizeof(tab_lds<TG>), stream, P);
+  if (P.frames && P.cap) hipLaunchKernelGGL(k_table_emit, dim3((uint32_t)g.R), dim3(256), 0, stream, P);
+  return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
+}
+
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
                         const xyws_carry* cin, xyws_carry* cout, xyws_frame* frames, uint64_t cap,
                         uint64_t* nframes, uint32_t opts, hipStream_t stream) {
@@ -3077,8 +3187,10 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   constexpr uint32_t RUN_MODES = XYWS_OPT_PARSE_ONLY | XYWS_OPT_WG512 | XYWS_OPT_DIAG | XYWS_OPT_TEST_GIVEUP |
                                  XYWS_OPT_STEAL | XYWS_OPT_TEST_STEAL | XYWS_OPT_RUNS | XYWS_OPT_NO_LATTICE |
                                  XYWS_OPT_RUNS_NOWAIT | XYWS_OPT_WG1024 | XYWS_OPT_NO_LATENTRY;
-  const bool want_lat = !(opts & (RUN_MODES | XYWS_OPT_NO_LATDEC)) &&
+  const bool want_lat = !(opts & (RUN_MODES | XYWS_OPT_NO_LATDEC | XYWS_OPT_TABLE)) &&
                         ((opts & XYWS_OPT_LATTICE) || (!small && lattice_preferred(s)));
+  const bool want_tab = !want_lat && !(opts & (RUN_MODES | XYWS_OPT_NO_TABLE | XYWS_OPT_LATTICE)) &&
+                        ((opts & XYWS_OPT_TABLE) || (!small && table_preferred(s, hi - lo)));
   const bool mid = !small && !(opts & (XYWS_OPT_WG512 | XYWS_OPT_WG1024)) &&
                    ((opts & XYWS_OPT_WG256) || mid_preferred(s, hi - lo));
   const bool wg512 = !small && !mid && !(opts & XYWS_OPT_WG1024) && ((opts & XYWS_OPT_WG512) || wg512_preferred(s, hi - lo));
@@ -3151,7 +3263,35 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     P.fst = static_cast<uint64_t*>(s->fmem);
     P.rcap = rc_n;
   }
-  if (want_lat) {
+  if (want_tab) {
+    // the table decoder (index, stream, descriptors); the run decoder after it
+    // reads the redirect record (the lattice scratch's) and takes what it left
+    tab_geom g;
+    const bool fits = small ? tab_geometry<G_TAB_SMALL>(s, hi, true, g) : tab_geometry<G_TAB>(s, hi, false, g);
+    if (fits) {
+      const bool capt = cs != hipStreamCaptureStatusNone;
+      if (const int rc = lat_grow(s, 1, capt)) return rc;
+      uint64_t doff, loff;
+      if (const int rc = tab_grow(s, tab_bytes(g, &doff, &loff), capt)) return rc;
+      run_params PT = P;
+      uint8_t* tm = static_cast<uint8_t*>(s->tmem);
+      PT.lat = static_cast<uint64_t*>(s->lmem);
+      PT.tctl = reinterpret_cast<uint64_t*>(tm);
+      PT.trec = reinterpret_cast<uint64_t*>(tm + 8 * TW_WORDS);
+      PT.tdesc = reinterpret_cast<uint4*>(tm + doff);
+      PT.tlist = reinterpret_cast<xyws_frame*>(tm + loff);
+      PT.trcap = g.rcap;
+      PT.tspr = g.spr;
+      PT.rbytes = g.spr * (small ? G_TAB_SMALL::SEG : G_TAB::SEG);
+      PT.nruns = (uint32_t)g.R;
+      PT.pfs = 0;
+      const int rc = small ? launch_table<G_SMALL, G_TAB_SMALL>(PT, g, 64, stream)
+                           : launch_table<G_PROD, G_TAB>(PT, g, (uint64_t)s->ncu, stream);
+      if (rc) return rc;
+      P.lat = PT.lat;
+      P.opts |= XYWS_OPT_REDIRECT;
+    }
+  } else if (want_lat) {
     // the lattice decoder first; the run decoder after it reads its redirect record
     const bool two = !small && (opts & XYWS_OPT_LATX_2WG);
     const uint64_t lseg = small ? G_LAT_SMALL::SEG : two ? G_LAT2::SEG : G_LAT::SEG;
