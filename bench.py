@@ -614,8 +614,13 @@ def main():
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
+        # gloo (host TCP): the ranks share nothing on the data path — each
+        # decodes its own frames in its own HBM — so the only cross-rank
+        # traffic is the timing barrier, the max over ranks and the parity
+        # AND, a few bytes on the host after torch.cuda.synchronize(); no RCCL
+        # communicator is created
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")
 
     from xynet_amd import _lib, websocket as ws
     T = _lib.load_tools()
@@ -698,7 +703,7 @@ def main():
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = max_over_ranks(dist, torch, t1 - t0, "cuda")
+    elapsed = max_over_ranks(dist, torch, t1 - t0, "cpu")
     avg_ms = ev0.elapsed_time(ev1) / args.steps
     decoder = None  # which decoder served the timed steps (the decoder choice, xyws_stream.hip)
     if args.mode == "fused":
@@ -756,7 +761,7 @@ def main():
     value = args.steps * total_payload / elapsed / GIB
     algo_bytes = info["algo_bytes"] + (32 * info["nframes"] if args.frames else 0)  # + the descriptors
     achieved = algo_bytes / (avg_ms * 1e-3) / 1e9
-    parity_all = all_ranks(dist, torch, parity, "cuda") if dist else parity
+    parity_all = all_ranks(dist, torch, parity, "cpu") if dist else parity
 
     cpu = None
     host_rate = None
