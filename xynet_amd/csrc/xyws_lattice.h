@@ -85,6 +85,14 @@ using G_LAT = lgeom<1024, 15 * 8 * 1024, 1>;
 // (experiment, XYWS_OPT_LATX_2WG: 56 KiB segments for 7 data waves, two
 // 512-thread workgroups per CU)
 using G_LAT2 = lgeom<512, 7 * 8 * 1024, 2>;
+// (experiments: 15 data waves of K rows; XYWS_EXP_LATK=K in the environment)
+template <uint32_t K>
+using G_LATK = lgeom<1024, 15 * K * 1024, 1>;
+using G_LATH = G_LATK<4>;  // (XYWS_OPT_LATX_HALF: 60 KiB segments)
+// 75 KiB segments: the geometry for frames of 16 KiB and more (c3: 0.670 vs
+// 0.688 ms in 120 KiB segments, same box, r05l; c1/c2 measured no faster)
+using G_LAT5 = G_LATK<5>;
+constexpr uint64_t LAT5_MIN_FRAME = 16384;
 using G_LAT_SMALL = lgeom<64, 1024>;  // tests: 1 KiB segments, many segment boundaries
 
 template <class G>

@@ -67,7 +67,7 @@ int stream_scratch_unmask_counter(stream_scratch* s, bool capturing, uint32_t** 
 #define XYWS_OPT_LATX_NOCHK 0x8000000u  // experiment (lattice decoder): no check of lattice points 1 and 2 up front
 #define XYWS_OPT_TABLE 0x10000000u   // the table decoder (index + stream), whatever the decoder choice would take
 #define XYWS_OPT_NO_TABLE 0x20000000u  // never the table decoder
-// (0x40000000: free)
+#define XYWS_OPT_LATX_HALF 0x40000000u  // experiment (lattice decoder): 60 KiB segments (G_LATH)
 #define XYWS_OPT_RUNS 0x80000000u     // the run decoder, whatever the decoder choice would take
 #define XYWS_OPT_LATTICE 0x400u      // the lattice decoder first, whatever the decoder choice would take
 #define XYWS_OPT_NO_LATDEC 0x800u    // never the lattice decoder

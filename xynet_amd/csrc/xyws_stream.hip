@@ -54,6 +54,7 @@
 
 #include <cstring>
 #include <mutex>
+#include <cstdlib>
 
 #include "xyws_stream.h"
 #include "xyws_device.h"
@@ -3036,8 +3037,8 @@ int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
     uint64_t d, l;
     if (const int rc = tab_grow(s, tab_bytes(tg, &d, &l), false)) return rc;
   }
-  // the lattice decoder's (production geometry)
-  return lat_grow(s, (max_batch_bytes + 15 + G_LAT::SEG - 1) / G_LAT::SEG, false);
+  // the lattice decoder's (production geometries: the 75 KiB segments have the most)
+  return lat_grow(s, (max_batch_bytes + 15 + G_LAT5::SEG - 1) / G_LAT5::SEG, false);
 }
 
 int stream_scratch_stats(stream_scratch* s, uint64_t out[XYWS_NSTATS]) {
@@ -3293,10 +3294,24 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     }
   } else if (want_lat) {
     // the lattice decoder first; the run decoder after it reads its redirect record
+    static const int expk = [] {  // (A/B experiments only: rows per data wave)
+      const char* e = getenv("XYWS_EXP_LATK");
+      const int k = e ? atoi(e) : 0;
+      return k >= 3 && k <= 8 ? k : 0;
+    }();
     const bool two = !small && (opts & XYWS_OPT_LATX_2WG);
-    const uint64_t lseg = small ? G_LAT_SMALL::SEG : two ? G_LAT2::SEG : G_LAT::SEG;
+    const bool half = !small && !two && (opts & XYWS_OPT_LATX_HALF);
+    // (the previous call's frames all F bytes, F >= LAT5_MIN_FRAME: 75 KiB segments)
+    const bool big = s->pol_h && s->pol_h[3] && s->pol_h[2] == s->pol_h[3] && s->pol_h[3] >= LAT5_MIN_FRAME;
+    const int kx = small || two || half ? 0 : expk ? (expk == 8 ? 0 : expk) : big ? 5 : 0;
+    const uint64_t lseg = small ? G_LAT_SMALL::SEG : two ? G_LAT2::SEG : half ? G_LATH::SEG
+                          : kx ? 15ull * kx * 1024 : G_LAT::SEG;
     const uint64_t lnseg = (hi + lseg - 1) / lseg;
-    if (const int rc = lat_grow(s, lnseg, cs != hipStreamCaptureStatusNone)) return rc;
+    // (scratch for the smallest production segments whatever this call takes:
+    // a geometry switch between calls must not grow it, e.g. inside a timed
+    // loop or a capture)
+    const uint64_t lsz = small ? lnseg : (hi + G_LAT5::SEG - 1) / G_LAT5::SEG;
+    if (const int rc = lat_grow(s, lnseg > lsz ? lnseg : lsz, cs != hipStreamCaptureStatusNone)) return rc;
     run_params PL = P;
     // after a call the lattice decoder finished, no first-segment gate (its
     // speculative stores are undone as any others; breaks at frames 1 and 2
@@ -3312,6 +3327,12 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     const uint32_t grid = (uint32_t)(lnseg < maxg ? lnseg : maxg);
     const int rc = small ? launch_lattice<G_LAT_SMALL>(PL, grid, stream)
                    : two ? launch_lattice<G_LAT2>(PL, grid, stream)
+                   : half ? launch_lattice<G_LATH>(PL, grid, stream)
+                   : kx == 3 ? launch_lattice<G_LATK<3>>(PL, grid, stream)
+                   : kx == 4 ? launch_lattice<G_LATK<4>>(PL, grid, stream)
+                   : kx == 5 ? launch_lattice<G_LATK<5>>(PL, grid, stream)
+                   : kx == 6 ? launch_lattice<G_LATK<6>>(PL, grid, stream)
+                   : kx == 7 ? launch_lattice<G_LATK<7>>(PL, grid, stream)
                          : launch_lattice<G_LAT>(PL, grid, stream);
     if (rc) return rc;
     P.lat = PL.lat;
