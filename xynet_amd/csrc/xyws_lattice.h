@@ -185,22 +185,15 @@ XYWS_DEV void lat_wait_decided(const run_params& P, uint64_t E, uint64_t s, uint
 
 // XOR mask of the 16-byte chunk at segment offset a from the table: entry
 // `idx` and the one after it (a chunk meets at most two frames, F >= 16).
+// (every wave of a small-frame batch takes the second form on some lane: a
+// chunk meeting a frame boundary or a header; span_key16 keeps it short)
 XYWS_DEV u32x4 lat_mask(const uint4* tab, uint32_t nent, uint32_t idx, uint32_t a) {
   const uint4 g = tab[idx];
   if (g.x <= a && a + 16u <= g.y) return u32x4{g.z, g.z, g.z, g.z};
-  u32x4 m;
-  m.x = g.z & range_mask32(a, g.x, g.y);
-  m.y = g.z & range_mask32(a + 4, g.x, g.y);
-  m.z = g.z & range_mask32(a + 8, g.x, g.y);
-  m.w = g.z & range_mask32(a + 12, g.x, g.y);
+  u32x4 m = span_key16(a, g.x, g.y, g.z);
   if (idx + 1 < nent) {
     const uint4 n = tab[idx + 1];
-    if (n.x < a + 16u) {
-      m.x |= n.z & range_mask32(a, n.x, n.y);
-      m.y |= n.z & range_mask32(a + 4, n.x, n.y);
-      m.z |= n.z & range_mask32(a + 8, n.x, n.y);
-      m.w |= n.z & range_mask32(a + 12, n.x, n.y);
-    }
+    if (n.x < a + 16u) m |= span_key16(a, n.x, n.y, n.z);
   }
   return m;
 }
@@ -782,10 +775,7 @@ XYWS_DEV void lat_undo(const run_params& P, const lat_lds<G>& L, uint32_t tid, u
           en = uint4{lat_rel(ps, ss), lat_rel(end < P.hi ? end : P.hi, ss), aligned_key(h.key, ps, 0), 0u};
         }
       }
-      m.x |= en.z & range_mask32(a, en.x, en.y);
-      m.y |= en.z & range_mask32(a + 4, en.x, en.y);
-      m.z |= en.z & range_mask32(a + 8, en.x, en.y);
-      m.w |= en.z & range_mask32(a + 12, en.x, en.y);
+      m |= span_key16(a, en.x, en.y, en.z);
     }
     if (a >= from && a >= lo_r && a + 16u <= top) {
       // a whole chunk: four dwords (agent scope: past this CU's caches, which

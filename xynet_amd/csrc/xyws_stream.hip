@@ -600,14 +600,20 @@ struct seg_io {
 // ---------------------------------------------------------------- the chase
 // XOR words for the 16-byte chunk at segment offset a; entries are contiguous
 // frames sorted by start, g = the last entry starting at or before a.
-// Byte-select mask of the bytes of the word at segment offset a (a % 4 == 0)
-// that lie in [lo, hi).
-XYWS_DEV uint32_t range_mask32(uint32_t a, uint32_t lo, uint32_t hi) {
-  if (hi <= a || lo >= a + 4) return 0u;
-  const uint32_t l = lo > a ? lo - a : 0u;
-  const uint32_t h = hi - a < 4u ? hi - a : 4u;
-  const uint32_t mh = h >= 4 ? 0xFFFFFFFFu : ((1u << (8u * h)) - 1u);
-  return mh & ~((1u << (8u * l)) - 1u);
+
+// The key word kw on the bytes of the 16-byte chunk at a that lie in [lo, hi)
+// (segment-relative, any values): the byte mask as two 64-bit halves from the
+// clamped chunk-relative bounds (a few shifts, no per-dword range tests).
+XYWS_DEV u32x4 span_key16(uint32_t a, uint32_t lo, uint32_t hi, uint32_t kw) {
+  const uint32_t l = lo <= a ? 0u : lo - a >= 16u ? 16u : lo - a;
+  const uint32_t h = hi <= a ? 0u : hi - a >= 16u ? 16u : hi - a;
+  const uint64_t one = ~0ull;
+  // bytes [0, h) and [0, l) of the chunk, each as (low half, high half)
+  const uint64_t h0 = h >= 8 ? one : ~(one << (8u * h)), h1 = h >= 16 ? one : h > 8 ? ~(one << (8u * (h - 8))) : 0ull;
+  const uint64_t l0 = l >= 8 ? one : ~(one << (8u * l)), l1 = l >= 16 ? one : l > 8 ? ~(one << (8u * (l - 8))) : 0ull;
+  const uint64_t k = (uint64_t)kw | ((uint64_t)kw << 32);
+  const uint64_t m0 = (h0 & ~l0) & k, m1 = (h1 & ~l1) & k;
+  return u32x4{(uint32_t)m0, (uint32_t)(m0 >> 32), (uint32_t)m1, (uint32_t)(m1 >> 32)};
 }
 
 XYWS_DEV u32x4 chunk_xor(const fent* fl, uint32_t nfl, uint32_t g, uint32_t a) {
@@ -615,10 +621,7 @@ XYWS_DEV u32x4 chunk_xor(const fent* fl, uint32_t nfl, uint32_t g, uint32_t a) {
   for (uint32_t h = g; h < nfl; h++) {
     const fent f = fl[h];
     if (h != g && f.start >= a + 16) break;
-    w.x |= f.kw & range_mask32(a, f.ps, f.end);
-    w.y |= f.kw & range_mask32(a + 4, f.ps, f.end);
-    w.z |= f.kw & range_mask32(a + 8, f.ps, f.end);
-    w.w |= f.kw & range_mask32(a + 12, f.ps, f.end);
+    w |= span_key16(a, f.ps, f.end, f.kw);
   }
   return w;
 }
@@ -1229,22 +1232,13 @@ XYWS_DEV uint32_t boundary_chunks(lds_t<G>& L, const fent* fl, const uint2* rt, 
       }
       const fent f0 = fl[g0 + g];
       const fent f1 = fl[g0 + g + (gh > g ? 1u : 0u)];
-      m.x = f0.kw & range_mask32(a, f0.ps, f0.end);
-      m.y = f0.kw & range_mask32(a + 4, f0.ps, f0.end);
-      m.z = f0.kw & range_mask32(a + 8, f0.ps, f0.end);
-      m.w = f0.kw & range_mask32(a + 12, f0.ps, f0.end);
+      m = span_key16(a, f0.ps, f0.end, f0.kw);
       if (gh > g) {
-        m.x |= f1.kw & range_mask32(a, f1.ps, f1.end);
-        m.y |= f1.kw & range_mask32(a + 4, f1.ps, f1.end);
-        m.z |= f1.kw & range_mask32(a + 8, f1.ps, f1.end);
-        m.w |= f1.kw & range_mask32(a + 12, f1.ps, f1.end);
+        m |= span_key16(a, f1.ps, f1.end, f1.kw);
         // (a third frame starting in the chunk: frames under 16 bytes)
         for (uint32_t h = g0 + g + 2; h <= g0 + gh; h++) {
           const fent f = fl[h];
-          m.x |= f.kw & range_mask32(a, f.ps, f.end);
-          m.y |= f.kw & range_mask32(a + 4, f.ps, f.end);
-          m.z |= f.kw & range_mask32(a + 8, f.ps, f.end);
-          m.w |= f.kw & range_mask32(a + 12, f.ps, f.end);
+          m |= span_key16(a, f.ps, f.end, f.kw);
         }
       }
       if (!(mine && whole)) m = u32x4{0u, 0u, 0u, 0u};
@@ -1587,15 +1581,9 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
           const fent f1 = L.fl[two ? g + 1 : g];
           const u32x4 v = *reinterpret_cast<const u32x4*>(&L.seg[a]);
           u32x4 m;
-          m.x = f0.kw & range_mask32(a, f0.ps, f0.end);
-          m.y = f0.kw & range_mask32(a + 4, f0.ps, f0.end);
-          m.z = f0.kw & range_mask32(a + 8, f0.ps, f0.end);
-          m.w = f0.kw & range_mask32(a + 12, f0.ps, f0.end);
+          m = span_key16(a, f0.ps, f0.end, f0.kw);
           if (two) {
-            m.x |= f1.kw & range_mask32(a, f1.ps, f1.end);
-            m.y |= f1.kw & range_mask32(a + 4, f1.ps, f1.end);
-            m.z |= f1.kw & range_mask32(a + 8, f1.ps, f1.end);
-            m.w |= f1.kw & range_mask32(a + 12, f1.ps, f1.end);
+            m |= span_key16(a, f1.ps, f1.end, f1.kw);
           }
           const bool whole = a >= wl_r && a + 16 <= wh_r;
           if (!whole && a + 16 > wl_r && a < wh_r) edge |= 1u << k;
@@ -1781,9 +1769,12 @@ XYWS_DEV void scan_segment(const run_params& P, lds_t<G>& L, uint64_t ss, uint32
   // Candidate bits of chunk k (segment offset (k*NT + tid)*16: conflict-free
   // LDS reads), bit 8*b + h + i = byte b of dword i (h: a 4-bit lane of the
   // packed word).
+  // (32-bit bounds only: a 64-bit per-lane position here was a spilled
+  // value whose reload waited for the next segment's loads in flight)
+  const uint32_t rhi = rel_hi < 0xFFFFFFFFull ? (uint32_t)rel_hi : 0xFFFFFFFFu;
   auto chunk_bits = [&](uint32_t k, uint32_t h) -> uint32_t {
     const uint32_t a = (k * G::NT + tid) * 16u;
-    if (ss + a >= P.hi) return 0u;
+    if (a >= rhi) return 0u;
     const u32x4 v = *reinterpret_cast<const u32x4*>(L.seg + a);
     const uint32_t w4 = *reinterpret_cast<const uint32_t*>(L.seg + a + 16);
     uint32_t c = (cand_bytes(v.x, v.y, unm) >> (7 - h)) | (cand_bytes(v.y, v.z, unm) >> (6 - h)) |

@@ -546,18 +546,11 @@ XYWS_DEV u32x4 tab_mask(const uint4* tab, uint32_t nent, uint32_t a) {
   }
   const uint4 g = tab[lo];
   if (g.x <= a && a + 16u <= g.y) return u32x4{g.z, g.z, g.z, g.z};
-  u32x4 m;
-  m.x = g.z & range_mask32(a, g.x, g.y);
-  m.y = g.z & range_mask32(a + 4, g.x, g.y);
-  m.z = g.z & range_mask32(a + 8, g.x, g.y);
-  m.w = g.z & range_mask32(a + 12, g.x, g.y);
+  u32x4 m = span_key16(a, g.x, g.y, g.z);
   for (uint32_t j = lo + 1; j < nent; j++) {
     const uint4 n = tab[j];
     if (n.x >= a + 16u) break;
-    m.x |= n.z & range_mask32(a, n.x, n.y);
-    m.y |= n.z & range_mask32(a + 4, n.x, n.y);
-    m.z |= n.z & range_mask32(a + 8, n.x, n.y);
-    m.w |= n.z & range_mask32(a + 12, n.x, n.y);
+    m |= span_key16(a, n.x, n.y, n.z);
   }
   return m;
 }
