@@ -21,9 +21,11 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // A workgroup-uniform value read from LDS, moved to scalar registers (values
 // loaded from LDS live in VGPRs otherwise, where the store loops need them).
 XYWS_DEV uint32_t uniform32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// (the lane builtins return int: each half goes through uint32_t, or the low
+// half's bit 31 would sign-extend over the high half)
 XYWS_DEV uint64_t uniform64(uint64_t v) {
-  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
-         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
 }
 
 // Rotate a little-endian key word so byte t of the result XORs a byte whose
