@@ -700,17 +700,48 @@ struct iov_args {
   uint64_t len[XYWS_IOV_MAX];
   uint64_t off[XYWS_IOV_MAX];  // the piece's start in the staging buffer
 };
-// One piece per blockIdx.y; lane j of the grid copies bytes j, j + stride, ...
-// (a wave moves 64 consecutive bytes per instruction: one line either side,
-// whatever the two alignments). to_stage: pieces -> stage, else back.
+// One piece per blockIdx.y; lane i of the grid moves the i-th 16-byte line of
+// the destination: its source bytes are the two aligned source lines around
+// them and a funnel shift (lines holding no byte of the piece are not
+// loaded), whatever the two alignments; the lines at the piece's two ends
+// are stored bytewise. to_stage: pieces -> stage, else back.
+XYWS_DEV u32x4 iov_funnel(const u32x4& x, const u32x4& y, uint32_t sh) {
+  const uint64_t x0 = (uint64_t)x.x | ((uint64_t)x.y << 32), x1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
+  const uint64_t y0 = (uint64_t)y.x | ((uint64_t)y.y << 32);
+  const uint64_t y1 = (uint64_t)y.z | ((uint64_t)y.w << 32);
+  const bool h = sh >= 8;
+  const uint64_t a = h ? x1 : x0, b = h ? y0 : x1, c = h ? y1 : y0;
+  const uint32_t s8 = 8u * (sh & 7u);
+  const uint64_t r0 = s8 ? (a >> s8) | (b << (64u - s8)) : a, r1 = s8 ? (b >> s8) | (c << (64u - s8)) : b;
+  return u32x4{(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32)};
+}
 __global__ void __launch_bounds__(256) k_iov_copy(iov_args A, uint8_t* __restrict__ stage, int to_stage) {
   const uint32_t k = blockIdx.y;
-  uint8_t* p = A.base[k];
-  uint8_t* q = stage + A.off[k];
   const uint64_t n = A.len[k];
-  for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += (uint64_t)gridDim.x * 256) {
-    if (to_stage) q[j] = __builtin_nontemporal_load(p + j);
-    else __builtin_nontemporal_store(q[j], p + j);
+  if (!n) return;
+  uint8_t* sp = stage + A.off[k];
+  const uint8_t* src = to_stage ? A.base[k] : sp;
+  uint8_t* dst = to_stage ? sp : A.base[k];
+  const uint64_t d0 = reinterpret_cast<uintptr_t>(dst), d1 = d0 + n;
+  const uint64_t s0 = reinterpret_cast<uintptr_t>(src), s1 = s0 + n;
+  const uint64_t c0 = d0 & ~15ull, nch = (d1 - c0 + 15) / 16;
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < nch; c += (uint64_t)gridDim.x * 256) {
+    const uint64_t D = c0 + 16 * c, S = D - d0 + s0;  // (S: the source of byte D; wraps below s0 in line 0)
+    const uint64_t Sa = S & ~15ull;
+    const uint32_t sh = (uint32_t)(S & 15u);
+    const u32x4 x = Sa + 16 > s0 && Sa < s1 ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(Sa)) : z;
+    const u32x4 y = sh && Sa + 32 > s0 && Sa + 16 < s1
+                        ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(Sa + 16)) : z;
+    const u32x4 v = sh ? iov_funnel(x, y, sh) : x;
+    if (D >= d0 && D + 16 <= d1) {
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(D));
+    } else {
+      for (uint32_t t = 0; t < 16; t++) {
+        const uint32_t w = t < 4 ? v.x : t < 8 ? v.y : t < 12 ? v.z : v.w;  // (no dynamic index: no scratch)
+        if (D + t >= d0 && D + t < d1) *reinterpret_cast<uint8_t*>(D + t) = (uint8_t)(w >> (8u * (t & 3u)));
+      }
+    }
   }
 }
 
@@ -741,7 +772,7 @@ int xyws_decode_stream_iov(xyws_ctx* ctx, const xyws_iov* iov, uint32_t niov, co
   if (rc) return rc;
   if ((rc = ensure_iov(sl, total + 16, capt))) return rc;
   uint8_t* stage = static_cast<uint8_t*>(sl->iov_mem);
-  const dim3 grid((uint32_t)grid_for(longest, 256, 1024), niov ? niov : 1);
+  const dim3 grid((uint32_t)grid_for(longest / 16 + 2, 256, 1024), niov ? niov : 1);
   if (niov && total) {
     hipLaunchKernelGGL(k_iov_copy, grid, dim3(256), 0, s, A, stage, 1);
     if ((rc = hip_err(hipGetLastError()))) return rc;
