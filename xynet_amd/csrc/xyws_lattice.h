@@ -29,13 +29,17 @@
 //    counts in its 64-segment group. It does not wait for the segments before
 //    it: it stores every chunk below the first failing point KNOWN to it —
 //    its own, or LW_BRK as read one segment earlier (from one of 64 replicas).
-//    Only a workgroup's first segment is gated: it waits until every earlier
-//    segment has decided and reads LW_BRK fresh, so a batch that breaks near
-//    its start stores nothing wrong. Every later store is speculative: the
-//    workgroup records (segment, lattice index its stores stop at) and dumps
-//    the list to scratch at its end; the workgroup finishing the call undoes
-//    the stores past the final failing point (lat_undo: XOR is an
-//    involution, keys from the headers in memory). A workgroup whose list is
+//    Only a workgroup's first segment is gated (and not after a call the
+//    lattice decoder finished: XYWS_OPT_LAT_NOGATE): it waits until every
+//    earlier segment has decided and reads LW_BRK fresh, so a batch that
+//    breaks near its start stores nothing wrong. Every later store is
+//    speculative: the workgroup records (segment, lattice index its stores
+//    stop at); at its end a workgroup that knew of a failing point waits
+//    until every workgroup's loop has ended (LW_LOOPS: the failing point is
+//    final then) and undoes its own stores past it, the others dump their
+//    list to scratch and the workgroup finishing the call undoes those
+//    (lat_undo: XOR is an involution, keys from the headers in memory,
+//    which a decode never writes). A workgroup whose list is
 //    full (LAT_SLIST) stops speculating: it raises the failing point to the
 //    frame before its segment and the run decoder takes the rest.
 //  * Each lane XORs its 16-byte chunks with the keys of the (at most two)
