@@ -494,7 +494,7 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
     const __amdgpu_buffer_rsrc_t rs = lat_rsrc(P, (uint64_t)cur * G::SEG, G::SEG);
 #pragma unroll
     for (uint32_t k = 0; k < IO::K; k++)
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rs, OOB, k * 1024u, AUX_ST);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rs, OOB, k * 1024u, AUX_ST_STREAM);
   }
   // the data lanes number the lattice points of a segment among themselves
   const uint32_t dl = IO::CTRL ? tid - 64u : tid, NDL = IO::NDW * 64u;
@@ -688,7 +688,7 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
           *reinterpret_cast<u32x4*>(&L.seg[a]) = d;  // (stored bytewise below)
         }
         __builtin_amdgcn_raw_buffer_store_b128(d, rs, (whole && any) ? lane * 16u : OOB, IO::row(wave, k) * 1024u,
-                                               AUX_ST);
+                                               AUX_ST_STREAM);
         // (the store's data registers stay live past the next store)
         asm volatile("" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
         dprev = d;

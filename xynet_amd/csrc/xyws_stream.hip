@@ -81,10 +81,17 @@ constexpr uint32_t KHDR_127 = 2, KHDR_126 = 6, KHDR_7 = 8;
 constexpr uint32_t SPIN = 1u << 24;   // bounded spins (s_sleep 2 each: ~1 s)
 constexpr uint32_t OOB = 0x80000000u; // buffer offset past every range: load 0, store dropped
 constexpr int AUX_NT = 2;             // buffer cache policy: nontemporal (the streaming loads)
+// Policy of the payload stores: nontemporal (the run decoder); the lattice
+// and table decoders' streaming stores are sc1 | nt, written through past
+// the XCD's L2 (a decode never reads its stores back): c3 0.6712 -> 0.6512
+// ms, c1 0.1106 -> 0.1090 against nt alone, same box; sc1 alone 0.6564,
+// plain 0.7198 (profiles/r05y_store_policy_ab.txt); the run decoder measured
+// 0.5126 vs 0.5015 ms on c4 with them (r05z vs r05x) and keeps nt
 #ifndef XYWS_EXP_AUX_ST
 #define XYWS_EXP_AUX_ST 2
 #endif
-constexpr int AUX_ST = XYWS_EXP_AUX_ST;  // policy of the payload stores
+constexpr int AUX_ST = XYWS_EXP_AUX_ST;
+constexpr int AUX_ST_STREAM = 18;
 constexpr uint64_t PLEN_SPEC_MAX = 1ull << 46;
 constexpr uint32_t MAX_RUNS = 1024;
 // work stealing: a run is asked for its tail when it has at least this many

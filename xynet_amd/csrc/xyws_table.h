@@ -611,7 +611,7 @@ __global__ void __launch_bounds__(TG::NT) k_stream_table(run_params P) {
     const __amdgpu_buffer_rsrc_t rs = lat_rsrc(P, (uint64_t)cur * TG::SEG, TG::SEG);
 #pragma unroll
     for (uint32_t k = 0; k < K; k++)
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rs, OOB, k * 1024u, AUX_ST);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rs, OOB, k * 1024u, AUX_ST_STREAM);
   }
   while (cur != NONE32) {
     asm volatile("" : "+v"(tid));
@@ -681,7 +681,7 @@ __global__ void __launch_bounds__(TG::NT) k_stream_table(run_params P) {
         edge |= 1u << k;
         *reinterpret_cast<u32x4*>(&L.seg[a]) = d;  // (stored bytewise below)
       }
-      __builtin_amdgcn_raw_buffer_store_b128(d, rs, whole ? lane * 16u : OOB, (wave + NW * k) * 1024u, AUX_ST);
+      __builtin_amdgcn_raw_buffer_store_b128(d, rs, whole ? lane * 16u : OOB, (wave + NW * k) * 1024u, AUX_ST_STREAM);
       asm volatile("" ::"v"(dprev.x), "v"(dprev.y), "v"(dprev.z), "v"(dprev.w));
       dprev = d;
     }
