@@ -30,9 +30,12 @@ pytestmark = pytest.mark.gpu
 OPT_LATTICE = 0x400
 OPT_SMALL = 0x200
 OPT_TEST_LATSPEC = 0x10  # every store speculative: a broken lattice is undone by the end-of-work check
+OPT_TEST_LATDUMP = 0x20  # no workgroup undoes its own stores at its end: every list goes to the finisher
 MODES = {"lat": {"opts": OPT_LATTICE}, "lat1k": {"opts": OPT_LATTICE | OPT_SMALL},
          "lat_blind": {"opts": OPT_LATTICE | OPT_TEST_LATSPEC},
-         "lat1k_blind": {"opts": OPT_LATTICE | OPT_SMALL | OPT_TEST_LATSPEC}}
+         "lat1k_blind": {"opts": OPT_LATTICE | OPT_SMALL | OPT_TEST_LATSPEC},
+         "lat_blind_dump": {"opts": OPT_LATTICE | OPT_TEST_LATSPEC | OPT_TEST_LATDUMP},
+         "lat1k_blind_dump": {"opts": OPT_LATTICE | OPT_SMALL | OPT_TEST_LATSPEC | OPT_TEST_LATDUMP}}
 
 
 @pytest.fixture(scope="module")

@@ -30,6 +30,8 @@ OPT_LATTICE = 0x400        # the lattice decoder first (the run decoder after it
 OPT_NO_LATDEC = 0x800      # never the lattice decoder
 OPT_TABLE = 0x10000000     # the table decoder (index + stream) whatever the decoder choice would take
 OPT_NO_TABLE = 0x20000000  # never the table decoder
+OPT_TEST_LATSPEC = 0x10    # tests (lattice decoder): every store speculative (undone at the end of the work)
+OPT_TEST_LATDUMP = 0x20    # tests (lattice decoder): every speculative-store list undone by the finisher
 # debug stats indices (xyws_stream.hip)
 ST_RUNS, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRAMES = range(8)
 ST_GIVEUP, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS = 32, 33, 34, 35, 36
@@ -139,6 +141,8 @@ def load():
     L.xyws_debug_stats.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
     L.xyws_debug_policy.restype = i32
     L.xyws_debug_policy.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
+    L.xyws_debug_lattice.restype = i32
+    L.xyws_debug_lattice.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
     L.xyws_debug_records.restype = C.c_int64
     L.xyws_debug_records.argtypes = [vp, vp, C.POINTER(C.c_uint64), u64]
     L.xyws_debug_table.restype = C.c_int64

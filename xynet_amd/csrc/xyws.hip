@@ -42,18 +42,22 @@
 // tiles of UNMASK_NT x UNMASK_U chunks of 16 bytes from one counter, one claim
 // ahead, and keep the next tile's nontemporal loads in flight while the
 // current tile is XORed and stored (a register double buffer): every CU
-// streams to the end of the range instead of a fixed share of it
-// (scripts/bw_probe7 on the c3 batch, R+W: the fixed 2048-block grid-stride
-// form 5.34 TB/s; claimed 64 KiB tiles of 1024 threads x 4 chunks, two
-// workgroups per CU, 6.42 TB/s — the probe's best, with 1024 x 8 x 1 at 6.40;
-// 256-thread tiles 5.0-5.7). The two edge chunks store only their in-range
-// bytes. The last workgroup out resets the counter. ctr == nullptr (a launch
+// streams to the end of the range instead of a fixed share of it. The stores
+// are sc1|nt (written through past the XCD's L2, as the lattice decoder's).
+// Geometry and store policy from scripts/bw_probe11 on the c3 batch, R+W
+// (profiles/r06_unmask_ab.txt): one 1024-thread workgroup per CU on 64 KiB
+// tiles with sc1|nt stores 6.75 TB/s; two per CU 6.31 (nt stores 6.22, the
+// round-3..5 form); 80 KiB tiles 6.65, 96 KiB 6.56, 128 KiB 6.49; 48 KiB
+// tiles two per CU 6.15. (Round 3: the fixed 2048-block grid-stride form
+// 5.34 TB/s, scripts/bw_probe7.) The two edge chunks store only their
+// in-range bytes. The last workgroup out resets the counter. ctr == nullptr (a launch
 // captured into a graph, or no scratch slot free for the stream): the same
 // loop over static tiles (workgroup b: tiles b, b + grid, ...), no state
 // outside the launch, so a replay may run on any stream, concurrently too.
 #define UNMASK_NT 1024u
 #define UNMASK_U 4u
-#define UNMASK_WPC 2u
+#define UNMASK_WPC 1u
+#define UNMASK_AUX_ST 18  // sc1 | nt
 __global__ void __launch_bounds__(UNMASK_NT) k_unmask_range(uint8_t* __restrict__ base, uint64_t lo, uint64_t hi,
                                                             uint32_t kw, uint32_t* __restrict__ ctr) {
   constexpr uint32_t TILE = UNMASK_NT * UNMASK_U;  // chunks per tile
@@ -114,7 +118,7 @@ __global__ void __launch_bounds__(UNMASK_NT) k_unmask_range(uint8_t* __restrict_
     if (tc << 4 >= lo && (tc + TILE) << 4 <= hi) {
 #pragma unroll
       for (uint32_t u = 0; u < UNMASK_U; u++) {
-        __builtin_amdgcn_raw_buffer_store_b128(d[u], w, t * 16u, u * UNMASK_NT * 16u, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(d[u], w, t * 16u, u * UNMASK_NT * 16u, UNMASK_AUX_ST);
         // (the store's data registers stay live past the next store)
         asm volatile("" ::"v"(d[u].x), "v"(d[u].y), "v"(d[u].z), "v"(d[u].w));
       }
@@ -124,7 +128,8 @@ __global__ void __launch_bounds__(UNMASK_NT) k_unmask_range(uint8_t* __restrict_
         const uint64_t c = tc + u * UNMASK_NT + t;  // absolute chunk
         const uint64_t a = c << 4;
         const bool whole = a >= lo && a + 16 <= hi;
-        __builtin_amdgcn_raw_buffer_store_b128(d[u], w, whole ? t * 16u : 0x80000000u, u * UNMASK_NT * 16u, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(d[u], w, whole ? t * 16u : 0x80000000u, u * UNMASK_NT * 16u,
+                                               UNMASK_AUX_ST);
         asm volatile("" ::"v"(d[u].x), "v"(d[u].y), "v"(d[u].z), "v"(d[u].w));
         if (!whole && c < c1) {  // an edge chunk: its in-range bytes
           for (uint32_t b = 0; b < 16; b++) {
@@ -506,9 +511,26 @@ int64_t xyws_debug_table(xyws_ctx* ctx, void* stream, uint64_t* out, uint64_t wo
   return XYWS_ERR_INVALID;
 }
 
+// Internal: the lattice decoder's device-side choice on `stream`: {the device
+// policy word (bit 63 a call finished, bits 48..55 its decoder, bits 0..47
+// the size all its frames had or 0), lattice calls handed whole to the run
+// decoder on that word, ... by the prologue's checks (first frame, lattice
+// points 1-2), lattice calls whose segment loops ran in 75 KiB segments, ...
+// in 120 KiB segments} (counts per stream slot, cumulative). Synchronizes the
+// device. out: 5 words.
+int xyws_debug_lattice(xyws_ctx* ctx, void* stream, uint64_t* out) {
+  if (!ctx || !out) return XYWS_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  device_guard g(ctx->device);
+  for (auto& sl : ctx->slot)
+    if (sl.bound && sl.stream == (hipStream_t)stream) return stream_scratch_lattice(&sl.ss, out);
+  return XYWS_ERR_INVALID;
+}
+
 // Internal: the decoder-choice words the last fused stream decode on `stream`
 // published ({epoch, batch bytes, smallest, largest last-frame size, decoder:
-// 0 runs / 1 sweep / 2 runs in 512-thread workgroups}). Synchronizes the device.
+// 0 or 2 the run decoder (2: 512-thread workgroups), 3 the lattice decoder,
+// 4 the table decoder}). Synchronizes the device.
 int xyws_debug_policy(xyws_ctx* ctx, void* stream, uint64_t* out) {
   if (!ctx || !out) return XYWS_ERR_INVALID;
   std::lock_guard<std::mutex> lk(ctx->mu);

@@ -63,12 +63,18 @@ constexpr uint64_t LAT_FMAX = 1ull << 40;   // (lattice arithmetic stays well in
 // lattice scratch (u64 words, zeroed at allocation)
 enum {
   LW_CNT = 0,      // u32 [0] claim counter, u32 [1] done count (reset by the finisher)
-  LW_EPOCH = 1,    // completed calls (a call runs with E = this + 1)
   LW_BRK = 2,      // ~(earliest failing lattice index) of this call, 0 = none (reset by the finisher)
   LW_UNMASK = 3,   // xyws_unmask's claim counter pair (u32 claims, u32 done; reset by its last workgroup)
   LW_W = 4,        // the decided prefix: every segment below it has published its result (reset by the finisher)
   LW_LOOPS = 5,    // workgroups whose segment loop has ended (reset by the finisher)
+  // one 16-byte granule, loaded by the prologue in one round trip:
+  LW_DPOL = 6,     // the device policy word of the previous call in the stream (dpol_publish)
+  LW_EPOCH = 7,    // completed calls (a call runs with E = this + 1)
   LW_REDIR = 8,    // redirect record for the run decoder: [0] state, [1] p, [2] frames before p
+  LW_NBAIL_POL = 12,  // calls handed whole to the run decoder on the device policy word (cumulative)
+  LW_NBAIL_HYP = 13,  // calls handed whole to the run decoder by the prologue's checks (cumulative)
+  LW_NLOOP_A = 14,    // calls whose segment loops ran in the large-frame geometry (cumulative)
+  LW_NLOOP_B = 15,    // ... in the default geometry (cumulative)
   LW_RCARRY = 16,  // the carry the run decoder starts from at p (8 words)
   LW_STAT = 32     // per segment: (E << 2) | LS_*
 };
@@ -77,41 +83,51 @@ constexpr uint32_t LAT_SLIST = 512;            // speculative stores a workgroup
 constexpr uint32_t LAT_NOCLAIM = 0x7FFFFFFFu;  // (no claim: the next segment after it is none)
 enum : uint64_t { RD_DONE = 0, RD_FULL = 1, RD_FROM = 2 };
 
-template <uint32_t NT_, uint32_t SEG_, uint32_t WPC_ = 1>
+template <uint32_t NT_, uint32_t SEG_>
 struct lgeom {
-  static constexpr uint32_t NT = NT_, SEG = SEG_, WPC = WPC_;  // WPC: workgroups per CU
+  static constexpr uint32_t NT = NT_, SEG = SEG_;
   static constexpr uint32_t TMAX = SEG_ / LAT_FMIN + 3;  // covering frame + lattice points
 };
 // 120 KiB segments: 8 rows of 1 KiB for each of the 15 data waves (wave 0 is
 // the control wave; no partial last round: every data wave's loads and stores
 // are unconditional), one 1024-thread workgroup per CU
-using G_LAT = lgeom<1024, 15 * 8 * 1024, 1>;
-// (experiment, XYWS_OPT_LATX_2WG: 56 KiB segments for 7 data waves, two
-// 512-thread workgroups per CU)
-using G_LAT2 = lgeom<512, 7 * 8 * 1024, 2>;
-// (experiments: 15 data waves of K rows; XYWS_EXP_LATK=K in the environment)
-template <uint32_t K>
-using G_LATK = lgeom<1024, 15 * K * 1024, 1>;
-using G_LATH = G_LATK<4>;  // (XYWS_OPT_LATX_HALF: 60 KiB segments)
-// 75 KiB segments: the geometry for frames of 16 KiB and more (c3: 0.670 vs
-// 0.688 ms in 120 KiB segments, same box, r05l; c1/c2 measured no faster)
-using G_LAT5 = G_LATK<5>;
+using G_LAT = lgeom<1024, 15 * 8 * 1024>;
+// 75 KiB segments (5 rows per data wave): the geometry for frames of 16 KiB
+// and more (c3: 0.670 vs 0.688 ms in 120 KiB segments, same box, r05l; rows
+// per data wave 3..8 swept in profiles/r05_lattice_rows_ab.txt; c1/c2
+// measured no faster in them). One kernel holds both loops and takes one by
+// the size of THIS call's first frame (the prologue's F), so the choice never
+// lags behind calls in flight.
+using G_LAT5 = lgeom<1024, 15 * 5 * 1024>;
 constexpr uint64_t LAT5_MIN_FRAME = 16384;
 using G_LAT_SMALL = lgeom<64, 1024>;  // tests: 1 KiB segments, many segment boundaries
 
-template <class G>
-struct __attribute__((aligned(16))) lat_lds {
-  // the segment, the 16 bytes after it, and the 20 bytes at the dword at or
-  // below the header of the frame covering its first bytes
-  uint8_t seg[G::SEG + 48];
-  uint4 tab[G::TMAX];        // frames overlapping the segment: {ps, end, kw, 0} segment-relative
+// The LDS layout of a kernel holding the loops of geometries GA and GB: the
+// larger segment and table (the scalar words first: the prologue writes them
+// before it knows which loop runs).
+static_assert(LW_DPOL == LW_DPOL_WORD && LW_EPOCH == LW_DPOL + 1 && LW_DPOL % 2 == 0, "one 16-byte granule");
+
+template <class GA, class GB>
+struct llay {
+  static_assert(GA::NT == GB::NT, "one workgroup size");
+  static constexpr uint32_t NT = GA::NT;
+  static constexpr uint32_t SEG = GA::SEG > GB::SEG ? GA::SEG : GB::SEG;
+  static constexpr uint32_t TMAX = GA::TMAX > GB::TMAX ? GA::TMAX : GB::TMAX;
+};
+template <class GL>
+struct __attribute__((aligned(256))) lat_lds {
   cstate S0;                 // the state at the batch start (carry)
-  uint64_t E, X0, F, kmax, c0, kbf;
+  uint64_t E, X0, F, kmax, c0, kbf, nseg;
   uint64_t gk;  // ~(the failing lattice index known to the control wave), 0 = none
-  uint32_t na, cur, nxt, brk, quit, done_last, nsl;
+  uint32_t na, cur, nxt, brk, quit, done_last, nsl, big, nogate;
   // speculatively stored segments of this workgroup and the lattice index
   // their stores stop at (checked once every earlier segment has decided)
   uint64_t sl_seg[LAT_SLIST], sl_k[LAT_SLIST];
+  uint4 tab[GL::TMAX];        // frames overlapping the segment: {ps, end, kw, 0} segment-relative
+  // the segment, the 16 bytes after it, and the 20 bytes at the dword at or
+  // below the header of the frame covering its first bytes (256-byte aligned:
+  // the rows' LDS bank pattern does not depend on the table's size)
+  alignas(256) uint8_t seg[GL::SEG + 48];
 };
 
 // Segment-relative clamp of an absolute position to [0, 2^32).
@@ -239,10 +255,14 @@ XYWS_DEV void lat_carried_frame(const run_params& P, const xyws_carry* cz) {
 // has exited): the call's outputs when every lattice point held, else the
 // redirect record for the run decoder launched after this kernel; then the
 // counters are reset and the epoch advances.
-template <class G>
-XYWS_DEV void lat_finish(const run_params& P, lat_lds<G>& L) {
+template <class LL>
+XYWS_DEV void lat_finish(const run_params& P, LL& L) {
   uint64_t* rd = P.lat + LW_REDIR;
   const xyws_carry* cz = P.cin_user ? P.cin_user : &k_zero_carry;
+  {
+    const uint32_t w = L.na == 2 ? LW_NBAIL_POL : L.na ? LW_NBAIL_HYP : L.big ? LW_NLOOP_A : LW_NLOOP_B;
+    st_store(P.lat + w, st_load(P.lat + w) + 1);
+  }
   if (L.na) {
     st_store(rd, RD_FULL);  // the run decoder decodes the whole batch
   } else {
@@ -278,8 +298,9 @@ XYWS_DEV void lat_finish(const run_params& P, lat_lds<G>& L) {
 #pragma unroll
       for (int i = 0; i < 8; i++) reinterpret_cast<uint64_t*>(&cinc)[i] = reinterpret_cast<const uint64_t*>(cz)[i];
       write_outputs(P, &cinc, total, S);  // (after every read of cz: the carry out may alias it)
+      dpol_publish(P, F, DEC_LATTICE);
       if (P.pol) {
-        const uint64_t v[5] = {L.E, P.hi - P.lo, F, F, 3};
+        const uint64_t v[5] = {L.E, P.hi - P.lo, F, F, DEC_LATTICE};
 #pragma unroll
         for (int i = 1; i < 5; i++) __hip_atomic_store(P.pol + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(P.pol, v[0], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -437,8 +458,8 @@ struct lat_clock {
       if (acc[i]) stat_add(P, 16 + i, acc[i]);
   }
 };
-template <class G, int ROLE>
-XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32_t ahead) {
+template <class G, int ROLE, class LL>
+XYWS_DEV void lat_loop(const run_params& P, LL& L, uint32_t tid0, uint32_t ahead) {
   using IO = lat_io<G>;
   constexpr bool CT = ROLE != LR_DATA, DT = ROLE != LR_CTRL;
   uint32_t tid = tid0;
@@ -735,8 +756,8 @@ XYWS_DEV void lat_loop(const run_params& P, lat_lds<G>& L, uint32_t tid0, uint32
 // stores stop at, goes to its slice of P.lsl when its work ends (n, then
 // {segment, index} pairs; LAT_LSW words per workgroup).
 constexpr uint32_t LAT_LSW = 1 + 2 * LAT_SLIST;
-template <class G>
-XYWS_DEV void lat_dump_list(const run_params& P, const lat_lds<G>& L, uint32_t tid) {
+template <class G, class LL>
+XYWS_DEV void lat_dump_list(const run_params& P, const LL& L, uint32_t tid) {
   const uint32_t n = L.nsl;
   uint64_t* q = P.lsl + (uint64_t)blockIdx.x * LAT_LSW;
   if (tid == 0) q[0] = n;
@@ -753,8 +774,8 @@ XYWS_DEV void lat_dump_list(const run_params& P, const lat_lds<G>& L, uint32_t t
 // masks again (XOR is an involution), each frame's key from its header in
 // memory (headers are never written by a decode). Rare: a lattice broken in
 // the middle of a batch, after the first segments.
-template <class G>
-XYWS_DEV void lat_undo(const run_params& P, const lat_lds<G>& L, uint32_t tid, uint64_t s, uint64_t kst, uint64_t kb) {
+template <class G, class LL>
+XYWS_DEV void lat_undo(const run_params& P, const LL& L, uint32_t tid, uint64_t s, uint64_t kst, uint64_t kb) {
   const uint64_t X0 = L.X0, F = L.F, kmax = L.kmax;
   const uint64_t ss = s * G::SEG;
   const uint32_t stop = (uint32_t)(X0 + kst * F - ss < G::SEG ? X0 + kst * F - ss : G::SEG);
@@ -810,82 +831,21 @@ XYWS_DEV void lat_undo(const run_params& P, const lat_lds<G>& L, uint32_t tid, u
   }
 }
 
-template <class G>
-__global__ void __launch_bounds__(G::NT)
-__attribute__((amdgpu_waves_per_eu(G::NT * G::WPC >= 256 ? G::NT * G::WPC / 256 : 1))) k_stream_lattice(run_params P) {
+// Polls of LW_LOOPS before a workgroup that knew of a failing point gives up
+// undoing its own stores and leaves its list to the finisher (every loop has
+// ended by the finisher's time, LW_BRK is final there): a wait bounded well
+// below anything a stalled grid could cost, and never an undo with a failing
+// point that may still move (workgroups of this grid may not be resident yet,
+// e.g. while a kernel on another stream holds CUs).
+constexpr uint32_t LAT_UNDO_POLLS = 2048;
+
+// Everything after the prologue, for the geometry it chose (every workgroup
+// the same: the choice is a function of the batch's first frame): the
+// segment loop, the end-of-work undo, the done count and the finisher.
+template <class G, class LL>
+XYWS_DEV void lat_body(const run_params& P, LL& L, uint32_t tid, uint32_t ahead) {
   using IO = lat_io<G>;
-  extern __shared__ __attribute__((aligned(16))) uint8_t xs_lds[];
-  lat_lds<G>& L = *reinterpret_cast<lat_lds<G>*>(xs_lds);
-  const uint32_t tid = threadIdx.x;
   uint32_t* cnt = reinterpret_cast<uint32_t*>(P.lat + LW_CNT);
-  uint32_t ahead = NONE32;  // claim lane: the segment claimed one iteration ahead
-  // (the prologue: the control lane's dependent round trips — the epoch and
-  // the carry, the first header, two lattice points. Issuing the static first
-  // segment's rows before it measured no faster: c1 0.1110 vs 0.1102 ms, c2
-  // 0.1245 vs 0.1246, same box, r05d)
-  if (tid == 0) {
-    L.E = st_load(P.lat + LW_EPOCH) + 1;
-    const xyws_carry* cz = P.cin_user ? P.cin_user : &k_zero_carry;
-    uint64_t c0 = 0;
-    const cstate S0 = initial_state(P, cz, c0);
-    uint32_t na = (S0.st & S_PARTIAL) || S0.X >= P.hi ? 1u : 0u;
-    uint64_t F = 0, kmax = 0;
-    if (!na) {
-      const hdr_info h = hdr_global(P, S0.X, NONE);
-      F = sat_add(h.hlen, h.plen);
-      if (!h.hlen || F < LAT_FMIN || F > LAT_FMAX) na = 1;
-      else kmax = (P.hi - S0.X + F - 1) / F;
-    }
-    // Lattice points 1 and 2 (X0 + F, X0 + 2F) from memory before anything is
-    // stored: a batch whose frames change size there (an irregular batch after
-    // regular ones) goes to the run decoder whole at once, at the cost of this
-    // workgroup's first rows (not a gated first round of every workgroup).
-    // (Not in the blind test mode, whose breaks at frame 1 exercise the undo.)
-    if (!na && kmax > 1 && !(P.opts & (XYWS_OPT_TEST_LATSPEC | XYWS_OPT_LATX_NOCHK))) {
-      const uint64_t dl = (P.hi + 3) & ~3ull;
-      uint32_t r[2][5];
-#pragma unroll
-      for (int j = 0; j < 2; j++) {
-        const uint64_t a = (S0.X + (j + 1) * F) & ~3ull;
-#pragma unroll
-        for (int i = 0; i < 5; i++) {
-          const uint64_t q = a + 4 * i;
-          r[j][i] = (j == 0 || kmax > 2) && q < dl ? *reinterpret_cast<const uint32_t*>(P.base + q) : 0u;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 2; j++) {
-        const uint64_t k = j + 1;
-        if (k >= kmax) break;
-        const uint64_t x = S0.X + k * F;
-        const uint32_t sh = (uint32_t)(x & 3);
-        uint32_t w[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) w[i] = __builtin_amdgcn_alignbyte(r[j][i + 1], r[j][i], sh);
-        const uint64_t room = P.hi - x;
-        const hdr_info h = parse_header_words(w, room < 16 ? (uint32_t)room : 16u);
-        const bool last = k + 1 == kmax;
-        const uint64_t fend = h.hlen ? sat_add(x + h.hlen, h.plen) : x;
-        const bool ok = h.hlen ? ((uint64_t)h.hlen + h.plen == F && h.plen < F) || (last && fend >= P.hi) : last;
-        if (!ok) na = 1;
-      }
-    }
-    L.S0 = S0;
-    L.c0 = c0;
-    L.X0 = S0.X;
-    L.F = F;
-    L.kmax = kmax;
-    L.na = na;
-    L.quit = 0;
-    L.nsl = 0;
-    // the first round is static (segment b, then b + grid: every workgroup's
-    // first segment, the one its gate holds, is among the first grid
-    // segments, so no gate waits on a segment that waits itself), then claims
-    // from the counter offset by 2 * grid (lat_loop)
-    L.cur = !na && blockIdx.x < P.nseg ? blockIdx.x : NONE32;
-  }
-  if (tid == IO::CLAIM) ahead = blockIdx.x - gridDim.x;  // (+ 2 * grid at its use: b + grid)
-  __syncthreads();
   if (!L.na) {
     if constexpr (IO::CTRL) {
       // (a wave-uniform branch: each loop is a scalar branch target)
@@ -897,28 +857,31 @@ __attribute__((amdgpu_waves_per_eu(G::NT * G::WPC >= 256 ? G::NT * G::WPC / 256 
       lat_loop<G, LR_ALL>(P, L, tid, ahead);
     }
     __syncthreads();
-    // A failing point known when this workgroup's work ends: wait until every
+    // A failing point known when this workgroup's work ends: once every
     // workgroup's segment loop has ended (LW_BRK final: a segment raises it
     // before it publishes, and no segment is decoded after the loops end; no
-    // loop waits for anything here) and undo this workgroup's own speculative
+    // loop waits for anything here) the workgroup undoes its own speculative
     // stores past it, all workgroups in parallel (a break near the batch start
-    // after an ungated first round: up to a segment per workgroup). A break
-    // raised later than that is the finisher's, from the dumped lists
-    // (emptied here once undone).
+    // after an ungated first round: up to a segment per workgroup). When the
+    // loops have not all ended within LAT_UNDO_POLLS polls, or the failing
+    // point was raised later, the list goes to the finisher, which undoes it
+    // with the final LW_BRK (dumped lists are emptied here once undone).
     // (L.quit: a failing point this workgroup knew of, its own or LW_BRK as
     // read during its loop: no extra load when none was)
     if (tid < 64) {
       uint64_t b = 0;
       if (tid == 0) __hip_atomic_fetch_add(P.lat + LW_LOOPS, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (L.quit && L.nsl) {
-        for (uint32_t it = 0; uniform64(st_load(P.lat + LW_LOOPS)) < gridDim.x; it++) {
-          if (it >= (1u << 20)) {
-            if (tid == 0) atomicOr(P.head + 1, 2u);
+        const uint32_t polls = (P.opts & XYWS_OPT_TEST_LATDUMP) ? 0u : LAT_UNDO_POLLS;
+        bool ended = false;
+        for (uint32_t it = 0; it < polls; it++) {
+          if (uniform64(st_load(P.lat + LW_LOOPS)) >= gridDim.x) {
+            ended = true;
             break;
           }
           __builtin_amdgcn_s_sleep(8);
         }
-        b = uniform64(st_load(P.lat + LW_BRK));
+        if (ended) b = uniform64(st_load(P.lat + LW_BRK));
       }
       if (tid == 0) L.kbf = b && L.nsl ? ~b : NONE;
     }
@@ -1000,5 +963,156 @@ __attribute__((amdgpu_waves_per_eu(G::NT * G::WPC >= 256 ? G::NT * G::WPC / 256 
     __hip_atomic_store(P.lgrp + g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid < LAT_NREP) __hip_atomic_store(P.lbrk + LAT_REPW * tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid != 0) return;
-  lat_finish<G>(P, L);
+  lat_finish(P, L);
+}
+
+// The kernel: GA's loop for batches whose first frame is at least
+// LAT5_MIN_FRAME bytes, GB's otherwise (GA == GB: one loop, the test
+// geometry). The segment count is the chosen geometry's (P.nseg from the host
+// is unused; the grid covers the smaller segments, workgroups past the
+// segment count exit after their done count).
+template <class GA, class GB>
+__global__ void __launch_bounds__(GB::NT)
+__attribute__((amdgpu_waves_per_eu(GB::NT >= 256 ? GB::NT / 256 : 1))) k_stream_lattice(run_params P0) {
+  using GL = llay<GA, GB>;
+  using IO = lat_io<GB>;
+  static_assert(lat_io<GA>::CLAIM == IO::CLAIM, "one claim lane");
+  extern __shared__ __attribute__((aligned(256))) uint8_t xs_lds[];
+  lat_lds<GL>& L = *reinterpret_cast<lat_lds<GL>*>(xs_lds);
+  const uint32_t tid = threadIdx.x;
+  uint32_t ahead = NONE32;  // claim lane: the segment claimed one iteration ahead
+  // (the prologue: the control lane's dependent round trips — {the epoch and
+  // the device policy word, the carry, the first header at the batch start},
+  // then two lattice points; a carried frame adds one for the first header.
+  // Issuing the static first segment's rows before it measured no faster: c1
+  // 0.1110 vs 0.1102 ms, c2 0.1245 vs 0.1246, same box, r05d)
+  if (tid == 0) {
+    // One round trip for the granule {device policy word, epoch}, the carry
+    // and the dwords at the batch start (the first frame's header when
+    // nothing is carried: the usual case), all issued before one wait.
+    const xyws_carry* cz = P0.cin_user ? P0.cin_user : &k_zero_carry;
+    xyws_carry cc;
+    uint32_t r0[5];
+    uint64_t dp, ep;
+    {
+      // (the granule first, inline asm without a wait: the compiler neither
+      // waits for it nor moves the plain loads before it; one wait for all)
+      u32x4 g;
+      asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(g) : "v"(P0.lat + LW_DPOL) : "memory");
+      uint64_t cw[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) cw[i] = reinterpret_cast<const uint64_t*>(cz)[i];
+      // (unconditional loads, addresses clamped to the batch's last dword:
+      // a branch per dword made the compiler wait after each)
+      const uint64_t a0 = P0.lo & ~3ull, dl = (P0.hi + 3) & ~3ull;
+#pragma unroll
+      for (int i = 0; i < 5; i++) {
+        const uint64_t q = a0 + 4 * i;
+        r0[i] = *reinterpret_cast<const uint32_t*>(P0.base + (q < dl ? q : dl - 4));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(g)::"memory");
+#pragma unroll
+      for (int i = 0; i < 5; i++)
+        if (a0 + 4 * i >= dl) r0[i] = 0u;
+      dp = (uint64_t)g.x | ((uint64_t)g.y << 32);
+      ep = (uint64_t)g.z | ((uint64_t)g.w << 32);
+#pragma unroll
+      for (int i = 0; i < 8; i++) reinterpret_cast<uint64_t*>(&cc)[i] = cw[i];
+    }
+    L.E = ep + 1;
+    // the previous call in this stream (LW_DPOL, its finisher's): after an
+    // irregular one the run decoder takes this batch whole at once (unless
+    // the caller forces the lattice), after one the lattice decoder finished
+    // the first segments are not gated
+    const bool dvalid = dp >> 63, dreg = (dp & ((1ull << 48) - 1)) >= LAT_FMIN;
+    const uint64_t ddec = (dp >> 48) & 0x7Fu;
+    uint32_t na = dvalid && !dreg && !(P0.opts & XYWS_OPT_LATTICE) ? 2u : 0u;
+    L.nogate = dvalid && dreg && ddec == DEC_LATTICE && !(P0.opts & XYWS_OPT_LAT_GATE) ? 1u : 0u;
+    uint64_t c0 = 0;
+    const cstate S0 = initial_state(P0, &cc, c0);
+    if (!na && ((S0.st & S_PARTIAL) || S0.X >= P0.hi)) na = 1u;
+    uint64_t F = 0, kmax = 0;
+    if (!na) {
+      hdr_info h;
+      if (S0.X == P0.lo) {
+        const uint32_t sh = (uint32_t)(P0.lo & 3);
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) w[i] = __builtin_amdgcn_alignbyte(r0[i + 1], r0[i], sh);
+        const uint64_t room = P0.hi - P0.lo;
+        h = parse_header_words(w, room < 16 ? (uint32_t)room : 16u);
+      } else {
+        h = hdr_global(P0, S0.X, NONE);
+      }
+      F = sat_add(h.hlen, h.plen);
+      if (!h.hlen || F < LAT_FMIN || F > LAT_FMAX) na = 1;
+      else kmax = (P0.hi - S0.X + F - 1) / F;
+    }
+    // Lattice points 1 and 2 (X0 + F, X0 + 2F) from memory before anything is
+    // stored: a batch whose frames change size there (an irregular batch after
+    // regular ones) goes to the run decoder whole at once, at the cost of this
+    // workgroup's first rows (not a gated first round of every workgroup).
+    // (Not in the blind test mode, whose breaks at frame 1 exercise the undo.)
+    if (!na && kmax > 1 && !(P0.opts & (XYWS_OPT_TEST_LATSPEC | XYWS_OPT_LATX_NOCHK))) {
+      const uint64_t dl = (P0.hi + 3) & ~3ull;
+      uint32_t r[2][5];
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const uint64_t a = (S0.X + (j + 1) * F) & ~3ull;
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          const uint64_t q = a + 4 * i;
+          r[j][i] = (j == 0 || kmax > 2) && q < dl ? *reinterpret_cast<const uint32_t*>(P0.base + q) : 0u;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const uint64_t k = j + 1;
+        if (k >= kmax) break;
+        const uint64_t x = S0.X + k * F;
+        const uint32_t sh = (uint32_t)(x & 3);
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) w[i] = __builtin_amdgcn_alignbyte(r[j][i + 1], r[j][i], sh);
+        const uint64_t room = P0.hi - x;
+        const hdr_info h = parse_header_words(w, room < 16 ? (uint32_t)room : 16u);
+        const bool last = k + 1 == kmax;
+        const uint64_t fend = h.hlen ? sat_add(x + h.hlen, h.plen) : x;
+        const bool ok = h.hlen ? ((uint64_t)h.hlen + h.plen == F && h.plen < F) || (last && fend >= P0.hi) : last;
+        if (!ok) na = 1;
+      }
+    }
+    // the loop's geometry: GA's segments for large frames
+    const bool big = GA::SEG != GB::SEG && !na && F >= LAT5_MIN_FRAME;
+    const uint64_t seg = big ? GA::SEG : GB::SEG;
+    const uint64_t nseg = (P0.hi + seg - 1) / seg;
+    L.nseg = nseg;
+    L.S0 = S0;
+    L.c0 = c0;
+    L.X0 = S0.X;
+    L.F = F;
+    L.kmax = kmax;
+    L.na = na;
+    L.quit = 0;
+    L.nsl = 0;
+    L.big = big ? 1u : 0u;
+    // the first round is static (segment b, then b + grid: every workgroup's
+    // first segment, the one its gate holds, is among the first grid
+    // segments, so no gate waits on a segment that waits itself), then claims
+    // from the counter offset by 2 * grid (lat_loop)
+    L.cur = !na && blockIdx.x < nseg ? blockIdx.x : NONE32;
+  }
+  if (tid == IO::CLAIM) ahead = blockIdx.x - gridDim.x;  // (+ 2 * grid at its use: b + grid)
+  __syncthreads();
+  run_params P = P0;
+  P.nseg = uniform64(L.nseg);
+  P.opts &= ~XYWS_OPT_LAT_NOGATE;
+  if (uniform32(L.nogate)) P.opts |= XYWS_OPT_LAT_NOGATE;
+  if constexpr (GA::SEG != GB::SEG) {
+    if (uniform32(L.big)) {
+      lat_body<GA>(P, L, tid, ahead);
+      return;
+    }
+  }
+  lat_body<GB>(P, L, tid, ahead);
 }

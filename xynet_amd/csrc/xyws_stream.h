@@ -37,6 +37,11 @@ uint32_t stream_scratch_error(stream_scratch* s, bool clear);
 int stream_scratch_stats(stream_scratch* s, uint64_t out[XYWS_NSTATS]);
 int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_runs);
 int64_t stream_scratch_table(stream_scratch* s, uint64_t* out, uint64_t words);
+// {the device policy word (HW_DPOL), lattice calls handed whole to the run
+// decoder on it, ... by the prologue's checks, lattice calls whose segment
+// loops ran in 75 KiB segments, ... in 120 KiB segments}; synchronizes the
+// device
+int stream_scratch_lattice(stream_scratch* s, uint64_t out[5]);
 // xyws_unmask's claim counter pair (u32 claims, u32 workgroups done; zeroed at
 // allocation, reset by the kernel's last workgroup) in this scratch
 int stream_scratch_unmask_counter(stream_scratch* s, bool capturing, uint32_t** out);
@@ -60,14 +65,13 @@ int stream_scratch_unmask_counter(stream_scratch* s, bool capturing, uint32_t** 
 #define XYWS_OPT_NO_LATTICE 0x200000u   // experiment (run decoder): no lattice passes (row table and walk only)
 #define XYWS_OPT_STEAL 0x400000u       // work stealing between runs (off by default: measured no faster on c1-c4)
 #define XYWS_OPT_TEST_STEAL 0x800000u  // tests: stealing on, every fourth run starts late, pieces of 1 segment and up
-#define XYWS_OPT_LAT_NOGATE 0x1000000u  // (set by stream_decode_fused only) the lattice decoder without the
+#define XYWS_OPT_LAT_NOGATE 0x1000000u  // (set by the lattice kernel only, from the device policy word) no
                                         // first-segment gate: the previous call on the stream was the lattice's
 #define XYWS_OPT_LAT_GATE 0x2000000u    // experiment (lattice decoder): the first-segment gate whatever the
                                         // previous call found
 #define XYWS_OPT_LATX_NOCHK 0x8000000u  // experiment (lattice decoder): no check of lattice points 1 and 2 up front
 #define XYWS_OPT_TABLE 0x10000000u   // the table decoder (index + stream), whatever the decoder choice would take
 #define XYWS_OPT_NO_TABLE 0x20000000u  // never the table decoder
-#define XYWS_OPT_LATX_HALF 0x40000000u  // experiment (lattice decoder): 60 KiB segments (G_LATH)
 #define XYWS_OPT_RUNS 0x80000000u     // the run decoder, whatever the decoder choice would take
 #define XYWS_OPT_LATTICE 0x400u      // the lattice decoder first, whatever the decoder choice would take
 #define XYWS_OPT_NO_LATDEC 0x800u    // never the lattice decoder
@@ -75,7 +79,8 @@ int stream_scratch_unmask_counter(stream_scratch* s, bool capturing, uint32_t** 
                                      // failing-point filter): a broken lattice is undone by the end-of-work check
 #define XYWS_OPT_WG256 0x8u  // the run decoder in four 256-thread workgroups per CU on 16 KiB segments
 #define XYWS_OPT_LATX_ONLY 0x80u  // timing experiment only (wrong bytes after a redirect): no run decoder after the lattice
-#define XYWS_OPT_LATX_2WG 0x20u  // experiment (lattice decoder): the two-workgroups-per-CU geometry (G_LAT2)
+#define XYWS_OPT_TEST_LATDUMP 0x20u  // tests (lattice decoder): a workgroup never undoes its own speculative
+                                    // stores at its end: every list goes to the finisher
 #define XYWS_OPT_LATX_NOWORK 0x40u  // timing experiment only (wrong bytes): the lattice decoder's data waves skip
                                     // the checks and the XOR (its data path and control alone)
 #define XYWS_OPT_REDIRECT 0x2000u    // (set by stream_decode_fused only) the run decoder after the lattice decoder:

@@ -362,14 +362,34 @@ XYWS_DEV void fs_note(const run_params& P, uint64_t fsmin, uint64_t fsmax) {
   __hip_atomic_fetch_max(hw + HW_FSMAX, fsmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_max(hw + HW_FSMIN, ~fsmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The device-resident copy of the decoder-choice words, written by the
+// workgroup finishing a call: bit 63 a call has finished, bits 48..55 its
+// decoder, bits 0..47 the size every last frame of the call had (0: mixed
+// sizes). In the run scratch's head (u64 HW_DPOL, zeroed at allocation) and
+// in the lattice scratch when the context has one (LW_DPOL, next to the
+// lattice epoch: xyws_lattice.h). The lattice decoder's prologue loads it
+// with its epoch, so its first-segment gate and its bail-out after an
+// irregular call follow the previous call in the stream, not the host's view
+// of the pinned words (which lags by the calls in flight).
+enum : uint64_t { DEC_RUNS = 0, DEC_RUNS512 = 2, DEC_LATTICE = 3, DEC_TABLE = 4 };
+constexpr uint32_t HW_DPOL = 77;
+constexpr uint32_t LW_DPOL_WORD = 6;  // (= LW_DPOL, xyws_lattice.h)
+XYWS_DEV void dpol_publish(const run_params& P, uint64_t F, uint64_t decoder) {
+  const uint64_t f = F < (1ull << 48) ? F : 0;
+  const uint64_t v = (1ull << 63) | (decoder << 48) | f;
+  st_store(reinterpret_cast<uint64_t*>(P.head) + HW_DPOL, v);
+  if (P.lat) st_store(P.lat + LW_DPOL_WORD, v);
+}
 // The finisher (lane 0): the call's frame-size range into the host-visible
 // policy slot {epoch, batch bytes, smallest, largest last-frame size, decoder}
-// and the words reset for the next call. Host memory: system-scope stores.
+// (and its device copy) and the words reset for the next call. Host memory:
+// system-scope stores.
 XYWS_DEV void pol_publish(const run_params& P, uint64_t E, uint64_t decoder) {
   uint64_t* hw = reinterpret_cast<uint64_t*>(P.head);
   const uint64_t mx = st_load(hw + HW_FSMAX), mn = ~st_load(hw + HW_FSMIN);
   st_store(hw + HW_FSMAX, 0);
   st_store(hw + HW_FSMIN, 0);
+  dpol_publish(P, mx && mn == mx ? mx : 0, decoder);
   if (!P.pol) return;
   const uint64_t v[5] = {E, P.hi - P.lo, mx ? mn : 0, mx, decoder};
 #pragma unroll
@@ -2709,7 +2729,7 @@ __device__ __attribute__((always_inline)) inline void finish_call(run_params P, 
       st_store(hw + HW_EMIT_FLAG, (walked || st_load(hw + HW_EMIT_SLOW)) ? 1u : 0u);
       st_store(hw + HW_EMIT_SLOW, 0);
     }
-    pol_publish(P, L.E, G::NT == 512 ? 2u : 0u);  // (2: the run decoder in 512-thread workgroups)
+    pol_publish(P, L.E, G::NT == 512 ? DEC_RUNS512 : DEC_RUNS);
     st_store(hw + HW_BAD, 0);
     st_store(hw + HW_TOTAL, 0);
     st_store(hw + HW_DONE, 0);
@@ -2932,7 +2952,7 @@ static int scratch_grow(stream_scratch* s, uint64_t runs) {
 // scratch and one result word per segment, all zeroed at allocation (epoch 0:
 // no result of any call).
 static uint64_t lat_max_grid(const stream_scratch* s) {
-  const uint64_t g = (uint64_t)s->ncu * 2;  // (G_LAT2: two workgroups per CU)
+  const uint64_t g = (uint64_t)s->ncu;  // (one workgroup per CU)
   return g > 64 ? g : 64;
 }
 static int lat_grow(stream_scratch* s, uint64_t segs, bool capturing) {
@@ -3057,6 +3077,20 @@ int64_t stream_scratch_table(stream_scratch* s, uint64_t* out, uint64_t words) {
   return hipMemcpy(out, s->tmem, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int64_t)n : XYWS_ERR_HIP;
 }
 
+int stream_scratch_lattice(stream_scratch* s, uint64_t out[5]) {
+  for (int i = 0; i < 5; i++) out[i] = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
+  if (s->mem && hipMemcpy(out, static_cast<uint8_t*>(s->mem) + 8 * HW_DPOL, 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return XYWS_ERR_HIP;
+  if (s->lmem) {
+    const uint32_t w[4] = {LW_NBAIL_POL, LW_NBAIL_HYP, LW_NLOOP_A, LW_NLOOP_B};
+    for (int i = 0; i < 4; i++)
+      if (hipMemcpy(out + 1 + i, static_cast<uint64_t*>(s->lmem) + w[i], 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return XYWS_ERR_HIP;
+  }
+  return XYWS_OK;
+}
+
 int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_recs) {
   if (!s->mem) return XYWS_ERR_INVALID;
   if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
@@ -3131,22 +3165,23 @@ static bool lattice_preferred(const stream_scratch* s) {
   return fsmax && fsmin == fsmax && fsmin >= LAT_FMIN;
 }
 
-template <class G>
+template <class GA, class GB>
 int launch_lattice(const run_params& P, uint32_t grid, hipStream_t stream) {
   static std::mutex mu;
   static bool done[64] = {};
+  using LL = lat_lds<llay<GA, GB>>;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return XYWS_ERR_HIP;
   {
     std::lock_guard<std::mutex> lk(mu);
     if (!done[dev]) {
-      if (hipFuncSetAttribute((const void*)k_stream_lattice<G>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sizeof(lat_lds<G>)) != hipSuccess)
+      if (hipFuncSetAttribute((const void*)k_stream_lattice<GA, GB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sizeof(LL)) != hipSuccess)
         return XYWS_ERR_HIP;
       done[dev] = true;
     }
   }
-  hipLaunchKernelGGL(k_stream_lattice<G>, dim3(grid), dim3(G::NT), sizeof(lat_lds<G>), stream, P);
+  hipLaunchKernelGGL((k_stream_lattice<GA, GB>), dim3(grid), dim3(GB::NT), sizeof(LL), stream, P);
   return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
 
@@ -3235,7 +3270,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   P.cin = reinterpret_cast<xyws_carry*>(m + 64);
   P.fst = nullptr; P.rcap = 0;
   P.pol = s->pol_d;
-  P.lat = nullptr;
+  P.lat = static_cast<uint64_t*>(s->lmem);  // (nullable: the device policy word's second copy)
   P.segb = (uint32_t)seg;
   P.tbias = 0;
   P.obias = 0;
@@ -3291,47 +3326,25 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
       P.opts |= XYWS_OPT_REDIRECT;
     }
   } else if (want_lat) {
-    // the lattice decoder first; the run decoder after it reads its redirect record
-    static const int expk = [] {  // (A/B experiments only: rows per data wave)
-      const char* e = getenv("XYWS_EXP_LATK");
-      const int k = e ? atoi(e) : 0;
-      return k >= 3 && k <= 8 ? k : 0;
-    }();
-    const bool two = !small && (opts & XYWS_OPT_LATX_2WG);
-    const bool half = !small && !two && (opts & XYWS_OPT_LATX_HALF);
-    // (the previous call's frames all F bytes, F >= LAT5_MIN_FRAME: 75 KiB segments)
-    const bool big = s->pol_h && s->pol_h[3] && s->pol_h[2] == s->pol_h[3] && s->pol_h[3] >= LAT5_MIN_FRAME;
-    const int kx = small || two || half ? 0 : expk ? (expk == 8 ? 0 : expk) : big ? 5 : 0;
-    const uint64_t lseg = small ? G_LAT_SMALL::SEG : two ? G_LAT2::SEG : half ? G_LATH::SEG
-                          : kx ? 15ull * kx * 1024 : G_LAT::SEG;
+    // the lattice decoder first; the run decoder after it reads its redirect
+    // record. Its segment geometry (75 KiB for frames of LAT5_MIN_FRAME and
+    // more, else 120 KiB), the first-segment gate and its bail-out after an
+    // irregular call are decided in the kernel (the batch's first frame, the
+    // device policy word HW_DPOL); the grid covers the smaller segments.
+    const uint64_t lseg = small ? G_LAT_SMALL::SEG : G_LAT5::SEG;
     const uint64_t lnseg = (hi + lseg - 1) / lseg;
-    // (scratch for the smallest production segments whatever this call takes:
-    // a geometry switch between calls must not grow it, e.g. inside a timed
-    // loop or a capture)
-    const uint64_t lsz = small ? lnseg : (hi + G_LAT5::SEG - 1) / G_LAT5::SEG;
-    if (const int rc = lat_grow(s, lnseg > lsz ? lnseg : lsz, cs != hipStreamCaptureStatusNone)) return rc;
+    if (const int rc = lat_grow(s, lnseg, cs != hipStreamCaptureStatusNone)) return rc;
     run_params PL = P;
-    // after a call the lattice decoder finished, no first-segment gate (its
-    // speculative stores are undone as any others; breaks at frames 1 and 2
-    // are caught before anything is stored)
     PL.opts &= ~XYWS_OPT_LAT_NOGATE;
-    if (s->pol_h && s->pol_h[0] && (s->pol_h[4] & 3) == 3 && !(opts & XYWS_OPT_LAT_GATE)) PL.opts |= XYWS_OPT_LAT_NOGATE;
     PL.lat = static_cast<uint64_t*>(s->lmem);
     PL.lgrp = PL.lat + LW_STAT + s->lmax_segs;
     PL.lbrk = PL.lat + lat_rep_off(s->lmax_segs);
     PL.lsl = PL.lat + lat_sl_off(s->lmax_segs);
-    PL.nseg = lnseg;
-    const uint64_t maxg = small ? 64 : (uint64_t)s->ncu * (two ? G_LAT2::WPC : G_LAT::WPC);
+    PL.nseg = lnseg;  // (the kernel counts the segments of the geometry it takes)
+    const uint64_t maxg = small ? 64 : (uint64_t)s->ncu;
     const uint32_t grid = (uint32_t)(lnseg < maxg ? lnseg : maxg);
-    const int rc = small ? launch_lattice<G_LAT_SMALL>(PL, grid, stream)
-                   : two ? launch_lattice<G_LAT2>(PL, grid, stream)
-                   : half ? launch_lattice<G_LATH>(PL, grid, stream)
-                   : kx == 3 ? launch_lattice<G_LATK<3>>(PL, grid, stream)
-                   : kx == 4 ? launch_lattice<G_LATK<4>>(PL, grid, stream)
-                   : kx == 5 ? launch_lattice<G_LATK<5>>(PL, grid, stream)
-                   : kx == 6 ? launch_lattice<G_LATK<6>>(PL, grid, stream)
-                   : kx == 7 ? launch_lattice<G_LATK<7>>(PL, grid, stream)
-                         : launch_lattice<G_LAT>(PL, grid, stream);
+    const int rc = small ? launch_lattice<G_LAT_SMALL, G_LAT_SMALL>(PL, grid, stream)
+                         : launch_lattice<G_LAT5, G_LAT>(PL, grid, stream);
     if (rc) return rc;
     P.lat = PL.lat;
     P.opts |= XYWS_OPT_REDIRECT;

@@ -520,7 +520,7 @@ __global__ void __launch_bounds__(G::NT, 1) k_stream_index(run_params P) {
   if (full && tid < rstar && fsr) fs_note(P, fsr, fsr);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0 && full) pol_publish(P, L.E, 4);
+  if (tid == 0 && full) pol_publish(P, L.E, DEC_TABLE);
 }
 
 // ---------------------------------------------------------------- the stream
