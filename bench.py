@@ -721,7 +721,8 @@ def main():
                  "cyc_pro_fill", "cyc_pro_scan", "cyc_pro_publish", "dense_no_entry", "dense_chase_fail",
                  "dense_mismatch", "dense_overflow", "giveups", "bridges", "steal_requests", "steals",
                  "stolen_segments", "cyc_dense_validate", "cyc_rows", "cyc_serial_chase",
-                 "lattice_entries", "s41", "s42", "s43", "s44", "s45", "cyc_stride_pass", "s47"]
+                 "lattice_entries", "cyc_scan_w0", "cyc_scan_bits", "cyc_scan_surv", "s44", "s45", "cyc_stride_pass",
+                 "s47"]
         for _ in range(2):
             dec.opts |= _lib.OPT_STATS
             dec.decode(bufs[0], cap=0, count=False, carry=False)

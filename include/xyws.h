@@ -152,6 +152,12 @@ int xyws_ctx_destroy(xyws_ctx* ctx);
  * uncaptured call first (or XYWS_ERR_CAPACITY). Calls on larger batches grow
  * scratch lazily. */
 int xyws_ctx_reserve(xyws_ctx* ctx, uint64_t max_batch_bytes, uint64_t max_frames);
+/* The staging buffer of xyws_decode_stream_iov for sequences of up to
+ * `max_total_bytes` in all, in the slots of the streams already used on the
+ * context and in one spare (as xyws_ctx_reserve's per-frame tables): with
+ * xyws_ctx_reserve(ctx, max_total_bytes, ...) before it, an iov decode that
+ * fits allocates nothing and can be captured into a hipGraph. */
+int xyws_ctx_reserve_iov(xyws_ctx* ctx, uint64_t max_total_bytes);
 /* Device-side error word of the last completed call (0 = none). Synchronizes
  * the context's device. */
 int xyws_ctx_last_device_error(xyws_ctx* ctx, uint32_t* out);
@@ -222,8 +228,9 @@ typedef struct xyws_iov {
  * order (piece k starts at the sum of the earlier pieces' lengths). Three
  * launches whatever niov (gather into the stream's staging buffer, one
  * decode, scatter back); the staging buffer grows to the largest total seen
- * (XYWS_ERR_CAPACITY under capture before it has). XYWS_OPT_SERIAL_SCAN is
- * refused (XYWS_ERR_INVALID). */
+ * (XYWS_ERR_CAPACITY under capture before it has, or before
+ * xyws_ctx_reserve_iov reserved it). XYWS_OPT_SERIAL_SCAN is refused
+ * (XYWS_ERR_INVALID). */
 int xyws_decode_stream_iov(xyws_ctx* ctx, const xyws_iov* iov, uint32_t niov,
                            const xyws_carry* dev_carry_in, xyws_carry* dev_carry_out,
                            xyws_frame* dev_frames, uint64_t cap, uint64_t* dev_nframes,

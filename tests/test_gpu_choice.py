@@ -53,8 +53,12 @@ def test_decoder_choice_follows_the_frames(ws):
     round 4's lattice attempt cost 54 us). Every call is checked against the
     reference's digests, whichever decoder ran."""
     from xynet_amd import _lib
-    seq = [("c3_bin_64k", 0), ("c3_bin_64k", 0), ("c3_bin_64k", 0), ("c4_mixed", 0), ("c4_mixed", _lib.OPT_RUNS),
-           ("c4_mixed", _lib.OPT_RUNS), ("c4_mixed", 0), ("c4_mixed", 0), ("c2_bin_256", 0), ("c2_bin_256", 0),
+    # (calls 4, 5: the run decoder with the hints a c3 history gives it, the
+    # one-pass entry scan off, so that they time what call 3 runs after its
+    # hand-over)
+    alone = _lib.OPT_RUNS | _lib.OPT_NO_BIGSCAN
+    seq = [("c3_bin_64k", 0), ("c3_bin_64k", 0), ("c3_bin_64k", 0), ("c4_mixed", 0), ("c4_mixed", alone),
+           ("c4_mixed", alone), ("c4_mixed", 0), ("c4_mixed", 0), ("c2_bin_256", 0), ("c2_bin_256", 0),
            ("c3_bin_64k", _lib.OPT_RUNS), ("c3_bin_64k", 0), ("c3_bin_64k", 0), ("c4_mixed", 0),
            ("c3_bin_64k", 0), ("c4_mixed", 0)]
     dec = ws.frame_decoder()
@@ -98,7 +102,7 @@ def test_decoder_choice_follows_the_frames(ws):
     assert used[4] in (0, 2) and used[5] in (0, 2)
     assert used[13] in (0, 2) and used[15] in (0, 2)
     assert min(ms[3], ms[13], ms[15]) <= 1.05 * min(ms[4], ms[5]) + 0.02, ms
-    # after c4's mixed sizes: the run decoder (the table decoder is opt-in)
+    # after c4's mixed sizes: the run decoder
     assert used[6] in (0, 2) and used[7] in (0, 2), used
     # c2 after c4: the run decoder, then the lattice
     assert used[8] in (0, 2) and pols[8][2] == pols[8][3] == 264 and used[9] == 3

@@ -25,10 +25,10 @@ OPT_WG512 = 0x40000         # two 512-thread workgroups per CU, 64 KiB segments
 OPT_WG256 = 0x8             # four 256-thread workgroups per CU, 16 KiB segments
 OPT_NO_LATDEC = 0x800       # the run decoder itself (equal frames would take the lattice decoder)
 OPT_LATTICE = 0x400         # the lattice decoder first whatever the previous call found (the bench's decoder)
-OPT_TABLE = 0x10000000      # the table decoder (index + stream) whatever the previous call found
+OPT_BIGSCAN = 0x4000000     # entry scans: one filter pass per segment, whatever the previous call found
 MODES = {"fused": {}, "serial": {"serial": True}, "runs1k": {"small_segments": True},
          "lat": {"opts": OPT_LATTICE},
-         "tab": {"opts": OPT_TABLE}, "tab1k": {"small_segments": True, "opts": OPT_TABLE},
+         "bigscan": {"opts": OPT_BIGSCAN | OPT_NO_LATDEC}, "runs1k_bigscan": {"small_segments": True, "opts": OPT_BIGSCAN},
          "wg512": {"opts": OPT_WG512 | OPT_NO_LATDEC}, "wg256": {"opts": OPT_WG256 | OPT_NO_LATDEC},
          "wrong_hint": {"opts": OPT_UNMASKED_HINT | OPT_NO_LATDEC},
          "runs1k_wrong_hint": {"small_segments": True, "opts": OPT_UNMASKED_HINT},
@@ -155,8 +155,8 @@ def test_stream_split_with_carry(ws, name, mode):
         assert [[x[0] + k, x[1] + k] + x[2:] for x in fb] == g["frames"][s["n1"]:]
 
 
-@pytest.mark.parametrize("mode", ["fused", "runs1k", "runs1k_giveup", "runs1k_steal", "runs1k_steal_giveup", "tab",
-                                  "tab1k"])
+@pytest.mark.parametrize("mode", ["fused", "runs1k", "runs1k_giveup", "runs1k_steal", "runs1k_steal_giveup",
+                                  "bigscan", "runs1k_bigscan"])
 def test_fuzz_random_streams_vs_oracle(ws, oracle, mode):
     """Random frame soups + random cut points, GPU vs oracle."""
     rng = streams.SplitMix(0xF022)
@@ -179,16 +179,15 @@ def test_fuzz_random_streams_vs_oracle(ws, oracle, mode):
             assert carry_list(dec.carry()) == carry_list(carry)
 
 
-@pytest.mark.parametrize("mode", ["fused", "tab", "tab1k"])
+@pytest.mark.parametrize("mode", ["fused", "bigscan", "runs1k_bigscan"])
 @pytest.mark.parametrize("fake", [0, 1, 2])
 def test_dense_frames_with_header_like_payloads(ws, oracle, fake, mode):
     """Many small frames (the decoder's dense pass: sub-block chases from
     speculated entries) whose wire payload bytes are themselves chains of
     plausible client headers, so that speculated entries land inside payloads
-    and the sequential repair of the dense pass runs (the table decoder: its
-    runs' entry scans land on fake chains, the hand-over check fails and the
-    run decoder takes the batch from there). GPU vs oracle: bytes, count,
-    descriptors."""
+    and the sequential repair of the dense pass runs (the one-pass entry
+    scans: chains of fake headers carried from segment to segment). GPU vs
+    oracle: bytes, count, descriptors."""
     rng = streams.SplitMix(0xDE5E + fake)
     out = bytearray()
     while len(out) < (3 << 20):
@@ -216,7 +215,7 @@ def test_dense_frames_with_header_like_payloads(ws, oracle, fake, mode):
     assert carry_list(dec.carry()) == carry_list(carry)
 
 
-@pytest.mark.parametrize("mode", ["fused", "runs1k", "runs1k_giveup", "tab", "tab1k"])
+@pytest.mark.parametrize("mode", ["fused", "runs1k", "runs1k_giveup", "bigscan", "runs1k_bigscan"])
 @pytest.mark.parametrize("kind", ["stride_fakes", "size_changes", "long_lengths", "segment_ends"])
 def test_stride_pass_adversarial(ws, oracle, mode, kind):
     """The run decoder's stride pass (lane i parses the header at X + i*F,
@@ -229,7 +228,7 @@ def test_stride_pass_adversarial(ws, oracle, mode, kind):
     count, descriptors, carry."""
     rng = streams.SplitMix(0x57D1 + len(kind))
     out = bytearray()
-    target = 3 << 20 if mode in ("fused", "tab") else 200000
+    target = 3 << 20 if mode in ("fused", "bigscan") else 200000
     while len(out) < target:
         if kind == "stride_fakes":
             plen = 100 + rng.below(300)
@@ -412,9 +411,9 @@ CONFIG_CASES = ([(n, "fused") for n in [
     "c4_mixed", "c5_shard0", "c5_shard1", "c5_shard4", "c5_shard5", "c5_shard6", "c5_shard7"]] +
     [(n, "lat") for n in ["c1_text_4k", "c2_bin_256", "c3_bin_64k", "c4_mixed", "c5_shard0", "c5_shard1",
                           "c5_shard2", "c5_shard3", "c5_shard4", "c5_shard5", "c5_shard6", "c5_shard7"]] +
-    [(n, "tab") for n in ["t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m", "c1_text_4k", "c2_bin_256", "c3_bin_64k",
+    [(n, "bigscan") for n in ["t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m", "c1_text_4k", "c2_bin_256", "c3_bin_64k",
                           "c4_mixed", "c5_shard0", "c5_shard3"]] +
-    [(n, "tab1k") for n in ["t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m"]] +
+    [(n, "runs1k_bigscan") for n in ["t_bin_64k_x64", "t_bin_256_x4096", "t_mixed_8m"]] +
     [(n, "wg512") for n in ["t_mixed_8m", "c1_text_4k", "c2_bin_256", "c3_bin_64k", "c4_mixed"]] +
     [(n, "wg256") for n in ["t_mixed_8m", "c1_text_4k", "c2_bin_256", "c4_mixed"]] +
     [(n, "wrong_hint") for n in ["t_bin_256_x4096", "c4_mixed"]] +
@@ -452,10 +451,6 @@ def test_config_batches(ws, oracle, name, mode):
         # the lattice held over the whole batch (policy word 4 = 3) on the
         # regular configs; c4 is handed to the run decoder at frame 1
         assert (decoder_policy(dec)[4] == 3) == (name != "c4_mixed"), decoder_policy(dec)
-    if mode == "tab":
-        # the table decoder covered the whole batch (policy word 4 = 4), but
-        # for c2, whose 4096 frames per run overflow the record lists
-        assert (decoder_policy(dec)[4] == 4) == (name != "c2_bin_256"), decoder_policy(dec)
     del buf, r
     torch.cuda.empty_cache()
 

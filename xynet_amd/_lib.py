@@ -28,8 +28,8 @@ OPT_TEST_STEAL = 0x800000
 OPT_RUNS = 0x80000000      # the run decoder whatever the decoder choice would take
 OPT_LATTICE = 0x400        # the lattice decoder first (the run decoder after it takes what it leaves)
 OPT_NO_LATDEC = 0x800      # never the lattice decoder
-OPT_TABLE = 0x10000000     # the table decoder (index + stream) whatever the decoder choice would take
-OPT_NO_TABLE = 0x20000000  # never the table decoder
+OPT_BIGSCAN = 0x4000000    # tests: the entry scans' one-pass filter whatever the previous call found
+OPT_NO_BIGSCAN = 0x40000000  # the entry scans' window-0 pass whatever the previous call found
 OPT_TEST_LATSPEC = 0x10    # tests (lattice decoder): every store speculative (undone at the end of the work)
 OPT_TEST_LATDUMP = 0x20    # tests (lattice decoder): every speculative-store list undone by the finisher
 # debug stats indices (xyws_stream.hip)
@@ -129,6 +129,8 @@ def load():
     L.xyws_ctx_destroy.argtypes = [vp]
     L.xyws_ctx_reserve.restype = i32
     L.xyws_ctx_reserve.argtypes = [vp, u64, u64]
+    L.xyws_ctx_reserve_iov.restype = i32
+    L.xyws_ctx_reserve_iov.argtypes = [vp, u64]
     L.xyws_ctx_last_device_error.restype = i32
     L.xyws_ctx_last_device_error.argtypes = [vp, C.POINTER(u32)]
     L.xyws_unmask.restype = i32
@@ -145,8 +147,6 @@ def load():
     L.xyws_debug_lattice.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
     L.xyws_debug_records.restype = C.c_int64
     L.xyws_debug_records.argtypes = [vp, vp, C.POINTER(C.c_uint64), u64]
-    L.xyws_debug_table.restype = C.c_int64
-    L.xyws_debug_table.argtypes = [vp, vp, C.POINTER(C.c_uint64), u64]
     L.xyws_decode_stream.restype = i32
     L.xyws_decode_stream.argtypes = [vp, vp, u64, vp, vp, vp, u64, vp, u32, vp]
     L.xyws_decode_stream_iov.restype = i32

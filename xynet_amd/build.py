@@ -24,7 +24,7 @@ TARGETS = {
     "libxyws.so": ["xyws.hip", "xyws_stream.hip", "xyws_frames.hip", "xyws_arena.hip", "xyws_shard.hip"],
     "libxyws_tools.so": ["xyws_tools.hip"],
 }
-DEPS = ["xyws_device.h", "xyws_stream.h", "xyws_ctx.h", "xyws_lattice.h", "xyws_table.h"]
+DEPS = ["xyws_device.h", "xyws_stream.h", "xyws_ctx.h", "xyws_lattice.h"]
 
 
 def _stale(out, srcs):

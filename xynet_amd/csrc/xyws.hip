@@ -389,6 +389,7 @@ int xyws_ctx_create(int device, xyws_ctx** out) {
   c->err = nullptr;
   c->reserve_bytes = 0;
   c->reserve_frames = 0;
+  c->reserve_iov = 0;
   c->stage = nullptr;
   c->stage_cap = 0;
   for (auto& st : c->arena_stream) st = nullptr;
@@ -462,6 +463,26 @@ int xyws_ctx_reserve(xyws_ctx* ctx, uint64_t max_batch_bytes, uint64_t max_frame
   return XYWS_OK;
 }
 
+int xyws_ctx_reserve_iov(xyws_ctx* ctx, uint64_t max_total_bytes) {
+  if (!ctx) return XYWS_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  device_guard g(ctx->device);
+  if (!g.ok) return XYWS_ERR_HIP;
+  const uint64_t bytes = max_total_bytes + 16;  // (xyws_decode_stream_iov's staging: total + 16)
+  if (bytes > ctx->reserve_iov) ctx->reserve_iov = bytes;
+  // the slots bound to a stream now and one spare (the one the next new
+  // stream binds), as xyws_ctx_reserve's per-frame tables; the others get
+  // theirs when a stream binds them (acquire_slot)
+  bool spare = true;
+  for (auto& sl : ctx->slot) {
+    const bool take = sl.bound || spare;
+    if (!sl.bound) spare = false;
+    if (take)
+      if (const int rc = ensure_iov(&sl, ctx->reserve_iov, false)) return rc;
+  }
+  return XYWS_OK;
+}
+
 int xyws_ctx_last_device_error(xyws_ctx* ctx, uint32_t* out) {
   if (!ctx || !out) return XYWS_ERR_INVALID;
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -499,18 +520,6 @@ int64_t xyws_debug_records(xyws_ctx* ctx, void* stream, uint64_t* out, uint64_t 
   return XYWS_ERR_INVALID;
 }
 
-// Internal: the table decoder's control words (64 u64: coverage, first run
-// not covered, ...), run bases (1024) and run records (16 u64 per run) of the
-// last call on `stream`; returns the words copied. Synchronizes the device.
-int64_t xyws_debug_table(xyws_ctx* ctx, void* stream, uint64_t* out, uint64_t words) {
-  if (!ctx || !out) return XYWS_ERR_INVALID;
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  device_guard g(ctx->device);
-  for (auto& sl : ctx->slot)
-    if (sl.bound && sl.stream == (hipStream_t)stream) return stream_scratch_table(&sl.ss, out, words);
-  return XYWS_ERR_INVALID;
-}
-
 // Internal: the lattice decoder's device-side choice on `stream`: {the device
 // policy word (bit 63 a call finished, bits 48..55 its decoder, bits 0..47
 // the size all its frames had or 0), lattice calls handed whole to the run
@@ -529,8 +538,8 @@ int xyws_debug_lattice(xyws_ctx* ctx, void* stream, uint64_t* out) {
 
 // Internal: the decoder-choice words the last fused stream decode on `stream`
 // published ({epoch, batch bytes, smallest, largest last-frame size, decoder:
-// 0 or 2 the run decoder (2: 512-thread workgroups), 3 the lattice decoder,
-// 4 the table decoder}). Synchronizes the device.
+// 0 or 2 the run decoder (2: 512-thread workgroups), 3 the lattice
+// decoder}). Synchronizes the device.
 int xyws_debug_policy(xyws_ctx* ctx, void* stream, uint64_t* out) {
   if (!ctx || !out) return XYWS_ERR_INVALID;
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -767,6 +776,26 @@ __global__ void __launch_bounds__(256) k_iov_copy(iov_args A, uint8_t* __restric
   }
 }
 
+// The buffer-sequence decode in pieces (xyws_decode_stream_iov): out ==
+// nullptr: *cnt = the stream's frame count before the call (0 for a fresh
+// stream); else *out = c's count minus it (the frames of the call).
+__global__ void k_iov_count(const xyws_carry* c, uint64_t* cnt, uint64_t* out) {
+  if (threadIdx.x) return;
+  const uint64_t v = c ? c->frames_total : 0;
+  if (out) *out = v - *cnt;
+  else *cnt = v;
+}
+// Pieces at least this long (empty ones not counted) are decoded in place one
+// by one when no descriptors are asked for (see xyws_decode_stream_iov): a
+// piece costs one decode's fixed cost instead of two more passes over its
+// bytes (~0.8 us per MiB). That cost follows the frames: ~20 us after a
+// call of equal frames (the lattice decoder), up to ~200 us after mixed
+// ones (the run decoder's entry scans). Measured (profiles/r06_iov_rate.jsonl,
+// gather/decode/scatter vs in place): c3 in 4 pieces 2.67 vs 0.72 ms, in 16
+// (128 MiB) 2.47 vs 0.97; c1 in 16 (16 MiB) 0.33 vs 0.42; c4 in 8 (128 MiB)
+// 1.46 vs 1.73.
+constexpr uint64_t IOV_PIECE_MIN_EQUAL = 64ull << 20, IOV_PIECE_MIN_MIXED = 256ull << 20;
+
 int xyws_decode_stream_iov(xyws_ctx* ctx, const xyws_iov* iov, uint32_t niov, const xyws_carry* dev_carry_in,
                            xyws_carry* dev_carry_out, xyws_frame* dev_frames, uint64_t cap,
                            uint64_t* dev_nframes, uint32_t opts, void* stream) {
@@ -792,6 +821,69 @@ int xyws_decode_stream_iov(xyws_ctx* ctx, const xyws_iov* iov, uint32_t niov, co
   scratch_slot* sl = nullptr;
   int rc = acquire_slot(ctx, s, capt, &sl);
   if (rc) return rc;
+  // Pieces in place: each piece decoded where it lies as the next batch of the
+  // stream, the carry chained from piece to piece on the device (a frame or
+  // header cut by a piece's end continues in the next, as across any two
+  // batches: the decode of a stream cut at any byte is the decode of the
+  // whole), so the bytes move once instead of three times (gather, decode,
+  // scatter). One decode per piece: for sequences of few large pieces
+  // without descriptors (the frame ordinals and offsets of later pieces
+  // would need the earlier pieces' counts on the host). Measured in DESIGN
+  // §4.4 (profiles/r06_iov_rate.jsonl).
+  uint32_t nz = 0;
+  uint64_t minlen = UINT64_MAX;
+  for (uint32_t k = 0; k < niov; k++)
+    if (iov[k].len) {
+      nz++;
+      if (iov[k].len < minlen) minlen = iov[k].len;
+    }
+  const bool desc = dev_frames && cap;
+  if (nz == 1 && !(opts & XYWS_OPT_IOV_STAGE)) {
+    // one non-empty piece: the decode of that buffer (offsets from its start,
+    // which is the sequence's: every piece before it is empty)
+    for (uint32_t k = 0; k < niov; k++)
+      if (iov[k].len) {
+        const uintptr_t addr = reinterpret_cast<uintptr_t>(iov[k].base);
+        return stream_decode_fused(&sl->ss, reinterpret_cast<uint8_t*>(addr & ~(uintptr_t)15), addr & 15,
+                                   (addr & 15) + iov[k].len, dev_carry_in, dev_carry_out, dev_frames, cap,
+                                   dev_nframes, opts, s);
+      }
+  }
+  const volatile uint64_t* pol = sl->ss.pol_h;  // (the stream's previous call: equal frames?)
+  const bool equal = pol && pol[3] && pol[2] == pol[3];
+  const uint64_t pmin = equal ? IOV_PIECE_MIN_EQUAL : IOV_PIECE_MIN_MIXED;
+  const bool pieces = nz > 1 && !desc && !(opts & XYWS_OPT_IOV_STAGE) &&
+                      ((opts & XYWS_OPT_IOV_PIECES) || minlen >= pmin);
+  if (pieces) {
+    // scratch: [0, 64) the carry between pieces, [64, 72) the frame count of
+    // the stream before the call (the count is the difference at the end)
+    if ((rc = ensure_iov(sl, 128, capt))) return rc;
+    xyws_carry* mid = static_cast<xyws_carry*>(sl->iov_mem);
+    uint64_t* base_cnt = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(sl->iov_mem) + 64);
+    xyws_carry* last_out = dev_carry_out ? dev_carry_out : mid;
+    if (dev_nframes) {
+      hipLaunchKernelGGL(k_iov_count, dim3(1), dim3(64), 0, s, dev_carry_in, base_cnt, (uint64_t*)nullptr);
+      if ((rc = hip_err(hipGetLastError()))) return rc;
+    }
+    uint32_t j = 0;
+    const xyws_carry* cin = dev_carry_in;
+    for (uint32_t k = 0; k < niov; k++) {
+      if (!iov[k].len) continue;
+      const bool lastp = ++j == nz;
+      xyws_carry* cout = lastp ? last_out : mid;
+      const uintptr_t addr = reinterpret_cast<uintptr_t>(iov[k].base);
+      uint8_t* b = reinterpret_cast<uint8_t*>(addr & ~(uintptr_t)15);
+      const uint64_t lo = addr & 15;
+      if ((rc = stream_decode_fused(&sl->ss, b, lo, lo + iov[k].len, cin, cout, nullptr, 0, nullptr, opts, s)))
+        return rc;
+      cin = cout;
+    }
+    if (dev_nframes) {
+      hipLaunchKernelGGL(k_iov_count, dim3(1), dim3(64), 0, s, last_out, base_cnt, dev_nframes);
+      if ((rc = hip_err(hipGetLastError()))) return rc;
+    }
+    return XYWS_OK;
+  }
   if ((rc = ensure_iov(sl, total + 16, capt))) return rc;
   uint8_t* stage = static_cast<uint8_t*>(sl->iov_mem);
   const dim3 grid((uint32_t)grid_for(longest / 16 + 2, 256, 1024), niov ? niov : 1);

@@ -48,6 +48,7 @@ struct xyws_ctx {
   std::mutex mu;
   uint32_t* err;  // device error word (serial / indexed modes)
   uint64_t reserve_bytes, reserve_frames;  // applied to every slot
+  uint64_t reserve_iov;                     // xyws_ctx_reserve_iov: the iov staging buffer of bound slots
   void* stage;          // xyws_mask_bytes: device copy of host bytes (under mu)
   uint64_t stage_cap;
   scratch_slot slot[XYWS_SLOTS];
@@ -125,6 +126,22 @@ inline int grid_for(uint64_t items, uint32_t per_block, uint32_t cap) {
   return (int)g;
 }
 
+// The iov staging buffer of at least `bytes` (ctx->mu held).
+inline int ensure_iov(scratch_slot* sl, uint64_t bytes, bool capture) {
+  if (bytes <= sl->iov_cap && sl->iov_mem) return XYWS_OK;
+  if (capture) return XYWS_ERR_CAPACITY;
+  uint64_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
+  void* mem = nullptr;
+  if (hipMalloc(&mem, cap) != hipSuccess) return XYWS_ERR_NOMEM;
+  if (sl->iov_mem) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(sl->iov_mem);
+  }
+  sl->iov_mem = mem;
+  sl->iov_cap = cap;
+  return XYWS_OK;
+}
+
 // The slot of `stream` (ctx->mu held).
 inline int acquire_slot(xyws_ctx* ctx, hipStream_t stream, bool capture, scratch_slot** out) {
   scratch_slot* pick = nullptr;
@@ -141,6 +158,10 @@ inline int acquire_slot(xyws_ctx* ctx, hipStream_t stream, bool capture, scratch
     }
     for (auto& sl : ctx->slot)
       if (!sl.bound) { pick = &sl; break; }
+  }
+  if (!pick->bound && ctx->reserve_iov && !capture) {
+    // (xyws_ctx_reserve_iov's staging buffer, as the per-frame tables below)
+    if (const int rc = ensure_iov(pick, ctx->reserve_iov, false)) return rc;
   }
   if (!pick->bound && ctx->reserve_frames && !capture) {
     // xyws_ctx_reserve's per-frame tables go to the slots streams bind (not
@@ -168,22 +189,6 @@ inline int ensure_aux(scratch_slot* sl, uint64_t bytes, bool capture) {
   }
   sl->aux_mem = mem;
   sl->aux_cap = cap;
-  return XYWS_OK;
-}
-
-// The iov staging buffer of at least `bytes` (ctx->mu held).
-inline int ensure_iov(scratch_slot* sl, uint64_t bytes, bool capture) {
-  if (bytes <= sl->iov_cap && sl->iov_mem) return XYWS_OK;
-  if (capture) return XYWS_ERR_CAPACITY;
-  uint64_t cap = bytes < (1u << 20) ? (1u << 20) : bytes;
-  void* mem = nullptr;
-  if (hipMalloc(&mem, cap) != hipSuccess) return XYWS_ERR_NOMEM;
-  if (sl->iov_mem) {
-    (void)hipDeviceSynchronize();
-    (void)hipFree(sl->iov_mem);
-  }
-  sl->iov_mem = mem;
-  sl->iov_cap = cap;
   return XYWS_OK;
 }
 

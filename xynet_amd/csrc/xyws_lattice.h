@@ -991,7 +991,7 @@ __attribute__((amdgpu_waves_per_eu(GB::NT >= 256 ? GB::NT / 256 : 1))) k_stream_
     // and the dwords at the batch start (the first frame's header when
     // nothing is carried: the usual case), all issued before one wait.
     const xyws_carry* cz = P0.cin_user ? P0.cin_user : &k_zero_carry;
-    xyws_carry cc;
+    carry_words cc;
     uint32_t r0[5];
     uint64_t dp, ep;
     {
@@ -999,9 +999,8 @@ __attribute__((amdgpu_waves_per_eu(GB::NT >= 256 ? GB::NT / 256 : 1))) k_stream_
       // waits for it nor moves the plain loads before it; one wait for all)
       u32x4 g;
       asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(g) : "v"(P0.lat + LW_DPOL) : "memory");
-      uint64_t cw[8];
 #pragma unroll
-      for (int i = 0; i < 8; i++) cw[i] = reinterpret_cast<const uint64_t*>(cz)[i];
+      for (int i = 0; i < 8; i++) cc.w[i] = reinterpret_cast<const uint64_t*>(cz)[i];
       // (unconditional loads, addresses clamped to the batch's last dword:
       // a branch per dword made the compiler wait after each)
       const uint64_t a0 = P0.lo & ~3ull, dl = (P0.hi + 3) & ~3ull;
@@ -1016,8 +1015,6 @@ __attribute__((amdgpu_waves_per_eu(GB::NT >= 256 ? GB::NT / 256 : 1))) k_stream_
         if (a0 + 4 * i >= dl) r0[i] = 0u;
       dp = (uint64_t)g.x | ((uint64_t)g.y << 32);
       ep = (uint64_t)g.z | ((uint64_t)g.w << 32);
-#pragma unroll
-      for (int i = 0; i < 8; i++) reinterpret_cast<uint64_t*>(&cc)[i] = cw[i];
     }
     L.E = ep + 1;
     // the previous call in this stream (LW_DPOL, its finisher's): after an
@@ -1029,7 +1026,7 @@ __attribute__((amdgpu_waves_per_eu(GB::NT >= 256 ? GB::NT / 256 : 1))) k_stream_
     uint32_t na = dvalid && !dreg && !(P0.opts & XYWS_OPT_LATTICE) ? 2u : 0u;
     L.nogate = dvalid && dreg && ddec == DEC_LATTICE && !(P0.opts & XYWS_OPT_LAT_GATE) ? 1u : 0u;
     uint64_t c0 = 0;
-    const cstate S0 = initial_state(P0, &cc, c0);
+    const cstate S0 = initial_state_w(P0, cc, c0);
     if (!na && ((S0.st & S_PARTIAL) || S0.X >= P0.hi)) na = 1u;
     uint64_t F = 0, kmax = 0;
     if (!na) {

@@ -21,8 +21,6 @@ struct stream_scratch {
   uint64_t* pol_d;
   void* lmem;           // lattice decoder: scratch words + one result word per segment
   uint64_t lmax_segs;
-  void* tmem;           // table decoder: control words, run records, segment descriptors, frame records
-  uint64_t tbytes;
 };
 
 void stream_scratch_init(stream_scratch* s, int device);
@@ -36,7 +34,6 @@ uint32_t stream_scratch_error(stream_scratch* s, bool clear);
 #define XYWS_NSTATS 48
 int stream_scratch_stats(stream_scratch* s, uint64_t out[XYWS_NSTATS]);
 int64_t stream_scratch_records(stream_scratch* s, uint64_t* out, uint64_t max_runs);
-int64_t stream_scratch_table(stream_scratch* s, uint64_t* out, uint64_t words);
 // {the device policy word (HW_DPOL), lattice calls handed whole to the run
 // decoder on it, ... by the prologue's checks, lattice calls whose segment
 // loops ran in 75 KiB segments, ... in 120 KiB segments}; synchronizes the
@@ -70,8 +67,11 @@ int stream_scratch_unmask_counter(stream_scratch* s, bool capturing, uint32_t** 
 #define XYWS_OPT_LAT_GATE 0x2000000u    // experiment (lattice decoder): the first-segment gate whatever the
                                         // previous call found
 #define XYWS_OPT_LATX_NOCHK 0x8000000u  // experiment (lattice decoder): no check of lattice points 1 and 2 up front
-#define XYWS_OPT_TABLE 0x10000000u   // the table decoder (index + stream), whatever the decoder choice would take
-#define XYWS_OPT_NO_TABLE 0x20000000u  // never the table decoder
+#define XYWS_OPT_IOV_PIECES 0x10000000u  // xyws_decode_stream_iov: the pieces in place one by one (no descriptors)
+#define XYWS_OPT_IOV_STAGE 0x20000000u   // xyws_decode_stream_iov: gather, decode, scatter whatever the pieces
+#define XYWS_OPT_BIGSCAN 0x4000000u  // tests (entry scans): one filter pass per segment, whatever the previous
+                                     // call found
+#define XYWS_OPT_NO_BIGSCAN 0x40000000u // experiment (entry scans): the window-0 pass whatever the previous call found
 #define XYWS_OPT_RUNS 0x80000000u     // the run decoder, whatever the decoder choice would take
 #define XYWS_OPT_LATTICE 0x400u      // the lattice decoder first, whatever the decoder choice would take
 #define XYWS_OPT_NO_LATDEC 0x800u    // never the lattice decoder

@@ -82,7 +82,7 @@ constexpr uint32_t SPIN = 1u << 24;   // bounded spins (s_sleep 2 each: ~1 s)
 constexpr uint32_t OOB = 0x80000000u; // buffer offset past every range: load 0, store dropped
 constexpr int AUX_NT = 2;             // buffer cache policy: nontemporal (the streaming loads)
 // Policy of the payload stores: nontemporal (the run decoder); the lattice
-// and table decoders' streaming stores are sc1 | nt, written through past
+// decoder's streaming stores are sc1 | nt, written through past
 // the XCD's L2 (a decode never reads its stores back): c3 0.6712 -> 0.6512
 // ms, c1 0.1106 -> 0.1090 against nt alone, same box; sc1 alone 0.6564,
 // plain 0.7198 (profiles/r05y_store_policy_ab.txt); the run decoder measured
@@ -248,6 +248,8 @@ struct run_params {
                                // find_entry's lattice entry)
   uint32_t dense0;             // run decoder: the previous call's frames were small and of mixed sizes:
                                // a run's first segment goes to the dense pass at once (no stride try)
+  uint32_t bigscan;            // entry scans: the previous call's frames had mixed sizes, some large
+                               // (find_entry: no window-0 pass, undecided chains carried forward)
   xyws_carry* cin;        // private snapshot of it, written by run 0 (finish/emit read it)
   xyws_carry* cout;
   xyws_frame* frames;
@@ -279,14 +281,6 @@ struct run_params {
   uint64_t* lsl;   // lattice decoder: the workgroups' speculative-store lists (LAT_LSW words each)
   uint32_t segb;
   uint64_t tbias, obias;
-  // table decoder (xyws_table.h): control words, run records, segment
-  // descriptors (TD_W granules each), frame records (trcap per run),
-  // segments per run range
-  uint64_t* tctl;
-  uint64_t* trec;
-  uint4* tdesc;
-  xyws_frame* tlist;
-  uint64_t trcap, tspr;
 };
 
 // (xyws_lattice.h, included below)
@@ -346,6 +340,8 @@ enum { ST_RUNS = 0, ST_NONE, ST_BAD, ST_REPAIR, ST_CUT, ST_SPIN, ST_SEGS, ST_FRA
        ST_T_PRO = 16, ST_T_MAIN, ST_T_WAIT, ST_T_FILL, ST_T_CHASE, ST_T_XOR, ST_T_TAIL, ST_T_PF, ST_T_CP,
        ST_P_FILL, ST_P_SCAN, ST_P_PUB, ST_D_NOENT, ST_D_CHASE, ST_D_MISMATCH, ST_D_OVF,
        ST_GIVEUP = 32, ST_BRIDGE, ST_STEAL_REQ, ST_STEAL_ACC, ST_STEAL_SEGS, ST_D_TVAL, ST_T_ROWS, ST_T_SER,
+       ST_X_W0 = 41, ST_X_BITS = 42, ST_X_SURV = 43,  // entry scan (lane 0): window 0 to its check; the
+                            // rest's candidate bits (from the segment's start); its survivors loop
        ST_T_STRIDE = 46,    // the run decoder's stride-pass time
        ST_P_LATTICE = 40 }; // runs whose entry the lattice gave
 XYWS_DEV void stat_add(const run_params& P, uint32_t i, uint64_t v) {
@@ -371,7 +367,7 @@ XYWS_DEV void fs_note(const run_params& P, uint64_t fsmin, uint64_t fsmax) {
 // with its epoch, so its first-segment gate and its bail-out after an
 // irregular call follow the previous call in the stream, not the host's view
 // of the pinned words (which lags by the calls in flight).
-enum : uint64_t { DEC_RUNS = 0, DEC_RUNS512 = 2, DEC_LATTICE = 3, DEC_TABLE = 4 };
+enum : uint64_t { DEC_RUNS = 0, DEC_RUNS512 = 2, DEC_LATTICE = 3 };
 constexpr uint32_t HW_DPOL = 77;
 constexpr uint32_t LW_DPOL_WORD = 6;  // (= LW_DPOL, xyws_lattice.h)
 XYWS_DEV void dpol_publish(const run_params& P, uint64_t F, uint64_t decoder) {
@@ -556,6 +552,58 @@ XYWS_DEV uint32_t cand_bytes(uint32_t w, uint32_t wn, bool unmasked) {
 XYWS_DEV bool cand_pair(uint32_t b0, uint32_t b1, bool unm) {
   return (b0 & 0x74u) == 0 && (b0 & 3u) != 3u && !((b0 & 0x08u) && !(b0 & 0x80u)) &&
          ((b1 >> 7) != 0) != unm;
+}
+
+// The carry as its 8 words in registers (xyws_carry: payload_remaining,
+// phase, frames_total, key[4] @24, hdr_len @28, hdr[14] @29): byte k by
+// shifts of constant amounts once unrolled, so no copy of the struct is
+// placed in scratch (the lattice decoder's prologue loads the words at once).
+struct carry_words {
+  uint64_t w[8];
+  XYWS_DEV uint32_t byte(uint32_t k) const { return (uint32_t)(w[k >> 3] >> (8u * (k & 7u))) & 0xFFu; }
+};
+XYWS_DEV cstate initial_state_w(const run_params& P, const carry_words& c, uint64_t& cnt) {
+  cstate s;
+  s.X = P.lo; s.cov_ps = P.lo; s.cov_start = P.lo; s.cov_kw = 0; s.cov_key = 0; s.st = S_NOCOV; s.pad = 0;
+  cnt = 0;
+  const uint64_t R = c.w[0];
+  if (R) {
+    const uint32_t k = (uint32_t)c.w[3];
+    s.X = sat_add(P.lo, R);
+    s.cov_kw = aligned_key(k, P.lo, c.w[1]);
+    s.cov_key = k;
+    s.st = S_CARRIED;
+    return s;
+  }
+  const uint32_t hl = c.byte(28);
+  if (hl) {
+    const uint32_t h0 = hl < XYWS_MAX_FRAME_HEADER_SIZE ? hl : XYWS_MAX_FRAME_HEADER_SIZE;
+    uint32_t w[4] = {0u, 0u, 0u, 0u}, n = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < XYWS_MAX_FRAME_HEADER_SIZE; i++) {
+      uint32_t b = 0;
+      bool have = true;
+      if (i < h0) b = c.byte(29 + i);
+      else if (P.lo + (i - h0) < P.hi) b = P.base[P.lo + (i - h0)];
+      else have = false;
+      if (have && n == i) {
+        w[i >> 2] |= b << (8u * (i & 3u));
+        n++;
+      }
+    }
+    const hdr_info h = parse_header_words(w, n);
+    if (!h.hlen) {  // still incomplete: the whole batch belongs to the header
+      s.st = S_NOCOV | S_PARTIAL | S_PARTCARRY;
+      return s;
+    }
+    s = frame_state(P.lo, h);
+    s.cov_ps = P.lo + (h.hlen - hl);
+    s.X = sat_add(s.cov_ps, h.plen);
+    s.cov_kw = aligned_key(h.key, s.cov_ps, 0);
+    s.st = S_HDRCARRY;
+    cnt = 1;
+  }
+  return s;
 }
 
 // State before the first byte of the batch, from the carry snapshot; cnt =
@@ -1733,19 +1781,21 @@ XYWS_DEV void run_chain(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_
 // Earliest position of run `run`'s range whose chain of KHDR headers is
 // plausible (lane 0 returns it through L.aux0; NONE if there is none). Leaves
 // the segment it was found in (L.aux1) in LDS.
-// 0: implausible, 1: plausible, 2: undecided (only when !mem: the chain
-// leaves the segment held in LDS)
+//
+// A candidate's chain from header position x with i headers verified (need:
+// the headers its length form asks for, set at the first): 0 implausible, 1
+// plausible, 2 undecided (only when !mem: its next header is not readable
+// from the LDS copy of [ss, ss + SEGX)); x, i and need are left where it
+// stopped.
 template <class G>
-XYWS_DEV uint32_t chain_plausible(const run_params& P, const lds_t<G>& L, uint64_t ss, uint64_t q, bool unm,
-                                  bool mem) {
-  uint64_t x = q;
-  uint32_t need = KHDR_7;
-  for (uint32_t i = 0; i < need; i++) {
+XYWS_DEV uint32_t chain_follow(const run_params& P, const lds_t<G>& L, uint64_t ss, uint64_t& x, uint32_t& i,
+                               uint32_t& need, bool unm, bool mem) {
+  for (; i < need; i++) {
     // a chain that ends with the batch counts after two verified headers (one
     // header whose length jumps past the batch end proves nothing: random
     // bytes 0xFF 0x00 0x00 ... pass as a 64-bit length below 2^46 often enough)
     if (x >= P.hi) return i >= 2;
-    if (!mem && x - ss + XYWS_MAX_FRAME_HEADER_SIZE > G::SEGX) return 2u;  // (x >= ss always)
+    if (!mem && (x < ss || x - ss + XYWS_MAX_FRAME_HEADER_SIZE > G::SEGX)) return 2u;
     const hdr_info h = hdr_at(P, L, ss, x, NONE);
     if (!h.hlen) return i >= 2;   // a header cut by the batch end
     if (!plausible(h, unm)) return 0u;
@@ -1756,6 +1806,13 @@ XYWS_DEV uint32_t chain_plausible(const run_params& P, const lds_t<G>& L, uint64
     x = sat_add(x + h.hlen, h.plen);
   }
   return 1u;
+}
+template <class G>
+XYWS_DEV uint32_t chain_plausible(const run_params& P, const lds_t<G>& L, uint64_t ss, uint64_t q, bool unm,
+                                  bool mem) {
+  uint64_t x = q;
+  uint32_t i = 0, need = KHDR_7;
+  return chain_follow<G>(P, L, ss, x, i, need, unm, mem);
 }
 
 // Second-level filter for the candidate at segment offset p (cheap, from LDS):
@@ -1775,7 +1832,8 @@ XYWS_DEV bool second_hop_ok(const run_params& P, const lds_t<G>& L, uint64_t ss,
 
 // Prologue scan of the segment at ss, in LDS (see find_entry): L.best = the
 // earliest offset whose chain of KHDR headers is plausible (0xFFFFFFFF: none).
-//  first for the segment's first NT chunks, then (no winner) for the rest:
+//  first for the segment's first NT chunks, then (no winner) for the rest
+//  (w0: both in one pass, after calls of large frames of mixed sizes):
 //  1. every lane filters its chunks: candidate bits (SWAR) and the cheap
 //     second-hop test; survivors go to an LDS list;
 //  2. survivors' chains, one per lane, followed in LDS; chains leaving the
@@ -1785,7 +1843,7 @@ XYWS_DEV bool second_hop_ok(const run_params& P, const lds_t<G>& L, uint64_t ss,
 // A list overflow (e.g. a stream of 2-byte frames) falls back to each lane
 // checking its own candidates in order through memory.
 template <class G>
-XYWS_DEV void scan_segment(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid, bool unm) {
+XYWS_DEV void scan_segment(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t tid, bool unm, bool w0) {
   const bool st_on = stats_on(P) && tid == 0;
   uint64_t tq = st_on ? __builtin_amdgcn_s_memtime() : 0, a_filt = 0, a_chk = 0, nwin = 0, nsurv = 0;
   if (tid == 0) { L.ucnt = 0; L.ovf = 0; }
@@ -1859,7 +1917,9 @@ XYWS_DEV void scan_segment(const run_params& P, lds_t<G>& L, uint64_t ss, uint32
   // Window 0 (the first NT chunks, 16 KiB for 1024 lanes) alone first: a
   // chain usually starts within one frame of the range start. Then the rest
   // of the segment in one pass, each lane's candidates in one loop (a wave
-  // iterates as often as its busiest lane).
+  // iterates as often as its busiest lane). (!w0: one pass for the whole
+  // segment: large frames leave window 0 empty, its check is one more round
+  // of barriers and LDS chains per segment.)
   if (tid == 0) L.ccnt = 0;
   __syncthreads();
   {
@@ -1870,16 +1930,27 @@ XYWS_DEV void scan_segment(const run_params& P, lds_t<G>& L, uint64_t ss, uint32
       survivor(tid * 16u + 4u * (t & 3u) + (t >> 3));
     }
   }
-  bool over = check();
-  if constexpr (G::CH > 1) if (!over && ss + G::NT * 16u < P.hi) {
-    if (tid == 0) L.ccnt = 0;
-    __syncthreads();
+  if (st_on) stat_add(P, ST_X_W0, __builtin_amdgcn_s_memtime() - tq);
+  const bool over = w0 ? check() : false;
+  bool rest = false;
+  if constexpr (G::CH > 1) rest = !over && ss + G::NT * 16u < P.hi;
+  if constexpr (G::CH > 1) if (rest) {
+    if (w0) {
+      if (tid == 0) L.ccnt = 0;
+      __syncthreads();
+    }
     // chunks 1..CH-1 packed two per word: m[j] holds chunks 2j+1 (h = 0) and 2j+2 (h = 4)
     constexpr uint32_t NM = G::CH / 2;
     uint32_t m[NM > 0 ? NM : 1];
 #pragma unroll
     for (uint32_t j = 0; j < NM; j++)
       m[j] = chunk_bits(2 * j + 1, 0) | (2 * j + 2 < G::CH ? chunk_bits(2 * j + 2, 4) : 0u);
+    uint64_t tb = 0;
+    if (st_on) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      tb = __builtin_amdgcn_s_memtime();
+      stat_add(P, ST_X_BITS, tb - tq);
+    }
     uint32_t any = 0;
 #pragma unroll
     for (uint32_t j = 0; j < NM; j++) any |= m[j];
@@ -1901,8 +1972,10 @@ XYWS_DEV void scan_segment(const run_params& P, lds_t<G>& L, uint64_t ss, uint32
       const uint32_t k = 2 * g + 1 + ((t >> 2) & 1u);
       survivor((k * G::NT + tid) * 16u + 4u * (t & 3u) + (t >> 3));
     }
+    if (st_on) stat_add(P, ST_X_SURV, __builtin_amdgcn_s_memtime() - tb);
     (void)check();
   }
+  if (!rest && !w0) (void)check();  // (window 0 was the whole pass: its own check)
   if (st_on) {
     stat_add(P, ST_P_TCOMP, a_filt); stat_add(P, ST_P_TCHECK, a_chk);
     stat_add(P, ST_P_WIN, nwin); stat_add(P, ST_P_CAND, nsurv); stat_add(P, ST_P_UND, L.ucnt);
@@ -1950,6 +2023,8 @@ template <class G>
 XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32_t tid, uint64_t rb,
                          uint64_t re) {
   const bool unm = (P.opts & XYWS_OPT_UNMASKED_HINT) != 0;
+  // (after a call of large frames of mixed sizes: no window-0 pass)
+  const bool big = P.bigscan != 0;
   if (re > P.hi) re = P.hi;
   if (tid == 0) L.aux0 = NONE;
   uint64_t tp = (stats_on(P) && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
@@ -1998,7 +2073,7 @@ XYWS_DEV void find_entry(const run_params& P, lds_t<G>& L, seg_io<G>& io, uint32
         break;
       }
     }
-    scan_segment<G>(P, L, ss, tid, unm);
+    scan_segment<G>(P, L, ss, tid, unm, !big);
     if (stats_on(P) && tid == 0) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       stat_add(P, ST_P_SCAN, t - tp);
@@ -2819,7 +2894,6 @@ __global__ void k_stream_empty(const xyws_carry* cin, xyws_carry* cout, uint64_t
 }
 
 #include "xyws_lattice.h"
-#include "xyws_table.h"
 
 constexpr uint64_t HEAD_BYTES = 1024;  // u32 [0] ticket, [1] error, [2..3] total, [4..5] epoch; bytes [64..128) carry,
                                        // [128..512) stats, [512..576) end-of-call words (HW_*)
@@ -2865,8 +2939,6 @@ void stream_scratch_init(stream_scratch* s, int device) {
   s->pol_d = nullptr;
   s->lmem = nullptr;
   s->lmax_segs = 0;
-  s->tmem = nullptr;
-  s->tbytes = 0;
   void* ph = nullptr;
   if (hipHostMalloc(&ph, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
     void* pd = nullptr;
@@ -2890,9 +2962,6 @@ void stream_scratch_free(stream_scratch* s) {
   if (s->lmem) (void)hipFree(s->lmem);
   s->lmem = nullptr;
   s->lmax_segs = 0;
-  if (s->tmem) (void)hipFree(s->tmem);
-  s->tmem = nullptr;
-  s->tbytes = 0;
   if (s->mem) (void)hipFree(s->mem);
   if (s->fmem) (void)hipFree(s->fmem);
   s->mem = nullptr;
@@ -2972,46 +3041,6 @@ static int lat_grow(stream_scratch* s, uint64_t segs, bool capturing) {
   return xyws_internal::zero_now(m, bytes) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
 
-// Table decoder geometry for a batch of hi bytes (from the 16-byte aligned
-// base): R run ranges of spr segments of TG::SEG bytes, trcap frame records
-// per run; false when the batch does not fit it (the run decoder then).
-struct tab_geom {
-  uint64_t nseg, spr, R, rcap;
-};
-template <class TG>
-static bool tab_geometry(const stream_scratch* s, uint64_t hi, bool small, tab_geom& g) {
-  g.nseg = (hi + TG::SEG - 1) / TG::SEG;
-  const uint64_t rmax = small ? 64 : (uint64_t)s->ncu;
-  g.spr = (g.nseg + rmax - 1) / rmax;
-  if (!g.spr) g.spr = 1;
-  g.R = (g.nseg + g.spr - 1) / g.spr;
-  const uint64_t rb = g.spr * TG::SEG;
-  g.rcap = rb / 1024 > 1024 ? rb / 1024 : 1024;
-  return g.spr <= TSPR_MAX && g.R >= 1 && g.R <= TAB_MAX_RUNS;
-}
-// Scratch: control words and per-run words (TW_WORDS, zeroed at allocation) |
-// run records | segment descriptors | frame records
-static uint64_t tab_bytes(const tab_geom& g, uint64_t* desc_off, uint64_t* list_off) {
-  const uint64_t ctl = 8 * TW_WORDS, rec = 8 * TR_WORDS * g.R;
-  const uint64_t desc = 16ull * TD_W * g.nseg;
-  *desc_off = (ctl + rec + 255) & ~255ull;
-  *list_off = (*desc_off + desc + 255) & ~255ull;
-  return *list_off + sizeof(xyws_frame) * g.R * g.rcap;
-}
-static int tab_grow(stream_scratch* s, uint64_t bytes, bool capturing) {
-  if (s->tmem && bytes <= s->tbytes) return XYWS_OK;
-  if (capturing) return XYWS_ERR_CAPACITY;
-  void* m = nullptr;
-  if (hipMalloc(&m, bytes) != hipSuccess) return XYWS_ERR_NOMEM;
-  if (s->tmem) {
-    (void)hipDeviceSynchronize();
-    (void)hipFree(s->tmem);
-  }
-  s->tmem = m;
-  s->tbytes = bytes;
-  return xyws_internal::zero_now(m, 8 * TW_WORDS) == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
-}
-
 int stream_scratch_unmask_counter(stream_scratch* s, bool capturing, uint32_t** out) {
   if (const int rc = lat_grow(s, 1, capturing)) return rc;
   *out = reinterpret_cast<uint32_t*>(static_cast<uint64_t*>(s->lmem) + LW_UNMASK);
@@ -3049,12 +3078,6 @@ int stream_scratch_reserve(stream_scratch* s, uint64_t max_batch_bytes) {
     if (n > runs) runs = n;
   }
   if (const int rc = scratch_grow(s, runs)) return rc;
-  // the table decoder's (production geometry)
-  tab_geom tg;
-  if (tab_geometry<G_TAB>(s, max_batch_bytes + 15, false, tg)) {
-    uint64_t d, l;
-    if (const int rc = tab_grow(s, tab_bytes(tg, &d, &l), false)) return rc;
-  }
   // the lattice decoder's (production geometries: the 75 KiB segments have the most)
   return lat_grow(s, (max_batch_bytes + 15 + G_LAT5::SEG - 1) / G_LAT5::SEG, false);
 }
@@ -3064,17 +3087,6 @@ int stream_scratch_stats(stream_scratch* s, uint64_t out[XYWS_NSTATS]) {
   if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
   return hipMemcpy(out, static_cast<uint8_t*>(s->mem) + 128, 8 * XYWS_NSTATS, hipMemcpyDeviceToHost) == hipSuccess
              ? XYWS_OK : XYWS_ERR_HIP;
-}
-
-// The table decoder's control words (64) and run records (TR_WORDS each), as
-// many words as fit `words`; returns the count copied. Synchronizes the device.
-int64_t stream_scratch_table(stream_scratch* s, uint64_t* out, uint64_t words) {
-  if (!s->tmem) return XYWS_ERR_INVALID;
-  if (hipDeviceSynchronize() != hipSuccess) return XYWS_ERR_HIP;
-  const uint64_t most = TW_WORDS + TAB_MAX_RUNS * TR_WORDS;
-  const uint64_t avail = s->tbytes / 8 < most ? s->tbytes / 8 : most;
-  const uint64_t n = words < avail ? words : avail;
-  return hipMemcpy(out, s->tmem, n * 8, hipMemcpyDeviceToHost) == hipSuccess ? (int64_t)n : XYWS_ERR_HIP;
 }
 
 int stream_scratch_lattice(stream_scratch* s, uint64_t out[5]) {
@@ -3129,6 +3141,7 @@ static bool mid_preferred(const stream_scratch* s, uint64_t len) {
   return fsmax && fsmax < WG512_MAX_FRAME && fsmin != fsmax && len <= (uint64_t)s->ncu * 32768;
 }
 constexpr uint64_t DENSE0_MAX_FRAME = 2048;
+constexpr uint64_t BIGSCAN_MIN_FRAME = 16384;
 static bool wg512_preferred(const stream_scratch* s, uint64_t len) {
   if (!s->pol_h) return false;
   const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
@@ -3143,21 +3156,6 @@ static bool wg512_preferred(const stream_scratch* s, uint64_t len) {
 // stream (XYWS_OPT_REDIRECT) and decodes what it left: nothing (it exits at
 // once), the batch from the first frame off the lattice, or all of it. Its
 // miss costs its loads of the batch's first segments.
-// The table decoder (xyws_table.h) would take a batch of at least
-// TAB_MIN_BATCH bytes after a call whose frames had mixed sizes, some of them
-// large (the largest last frame at least TAB_MIN_FRAME: config 4's 1 B - 1 MiB
-// frames). Measured slower than the run decoder on c4 (0.57 vs 0.51 ms: its
-// stream kernel takes 0.345 ms, at the lattice decoder's rate, but the index
-// kernel 0.22 ms, latency-bound on the entry scans and the header chases,
-// DESIGN §4.5), so it is opt-in (XYWS_OPT_TABLE) until the index is hidden.
-constexpr bool TAB_AUTO = false;
-constexpr uint64_t TAB_MIN_FRAME = 16384, TAB_MIN_BATCH = 64ull << 20;
-static bool table_preferred(const stream_scratch* s, uint64_t len) {
-  if (!TAB_AUTO || !s->pol_h || !s->pol_h[0] || len < TAB_MIN_BATCH) return false;
-  const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
-  return fsmax && fsmin != fsmax && fsmax >= TAB_MIN_FRAME;
-}
-
 static bool lattice_preferred(const stream_scratch* s) {
   if (!s->pol_h) return false;
   const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
@@ -3185,30 +3183,6 @@ int launch_lattice(const run_params& P, uint32_t grid, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
 }
 
-template <class G, class TG>
-int launch_table(const run_params& P, const tab_geom& g, uint64_t gcap, hipStream_t stream) {
-  static std::mutex mu;
-  static bool done[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return XYWS_ERR_HIP;
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    if (!done[dev]) {
-      if (hipFuncSetAttribute((const void*)k_stream_index<G, TG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sizeof(idx_lds<G>)) != hipSuccess ||
-          hipFuncSetAttribute((const void*)k_stream_table<TG>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sizeof(tab_lds<TG>)) != hipSuccess)
-        return XYWS_ERR_HIP;
-      done[dev] = true;
-    }
-  }
-  hipLaunchKernelGGL((k_stream_index<G, TG>), dim3((uint32_t)g.R), dim3(G::NT), sizeof(idx_lds<G>), stream, P);
-  const uint64_t grid = g.nseg < gcap ? g.nseg : gcap;
-  hipLaunchKernelGGL(k_stream_table<TG>, dim3((uint32_t)grid), dim3(TG::NT), sizeof(tab_lds<TG>), stream, P);
-  if (P.frames && P.cap) hipLaunchKernelGGL(k_table_emit, dim3((uint32_t)g.R), dim3(256), 0, stream, P);
-  return hipGetLastError() == hipSuccess ? XYWS_OK : XYWS_ERR_HIP;
-}
-
 int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t hi,
                         const xyws_carry* cin, xyws_carry* cout, xyws_frame* frames, uint64_t cap,
                         uint64_t* nframes, uint32_t opts, hipStream_t stream) {
@@ -3221,10 +3195,8 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
   constexpr uint32_t RUN_MODES = XYWS_OPT_PARSE_ONLY | XYWS_OPT_WG512 | XYWS_OPT_DIAG | XYWS_OPT_TEST_GIVEUP |
                                  XYWS_OPT_STEAL | XYWS_OPT_TEST_STEAL | XYWS_OPT_RUNS | XYWS_OPT_NO_LATTICE |
                                  XYWS_OPT_RUNS_NOWAIT | XYWS_OPT_WG1024 | XYWS_OPT_NO_LATENTRY;
-  const bool want_lat = !(opts & (RUN_MODES | XYWS_OPT_NO_LATDEC | XYWS_OPT_TABLE)) &&
+  const bool want_lat = !(opts & (RUN_MODES | XYWS_OPT_NO_LATDEC)) &&
                         ((opts & XYWS_OPT_LATTICE) || (!small && lattice_preferred(s)));
-  const bool want_tab = !want_lat && !(opts & (RUN_MODES | XYWS_OPT_NO_TABLE | XYWS_OPT_LATTICE)) &&
-                        ((opts & XYWS_OPT_TABLE) || (!small && table_preferred(s, hi - lo)));
   const bool mid = !small && !(opts & (XYWS_OPT_WG512 | XYWS_OPT_WG1024)) &&
                    ((opts & XYWS_OPT_WG256) || mid_preferred(s, hi - lo));
   const bool wg512 = !small && !mid && !(opts & XYWS_OPT_WG1024) && ((opts & XYWS_OPT_WG512) || wg512_preferred(s, hi - lo));
@@ -3290,6 +3262,15 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
     if (fsmax && fsmin != fsmax && fsmax < DENSE0_MAX_FRAME) P.dense0 = 1;
   }
+  // large frames of mixed sizes last call (some last frame of BIGSCAN_MIN_FRAME
+  // or more: config 4): the entry scans filter a whole segment in one pass (a
+  // range start usually lies inside a large frame: the first 16 KiB hold no
+  // entry, and their own round of checks cost 3.6 us per scanned segment, c4)
+  P.bigscan = (opts & XYWS_OPT_BIGSCAN) ? 1u : 0u;
+  if (s->pol_h && !(opts & XYWS_OPT_NO_BIGSCAN)) {
+    const uint64_t fsmin = s->pol_h[2], fsmax = s->pol_h[3];
+    if (fsmax && fsmin != fsmax && fsmax >= BIGSCAN_MIN_FRAME) P.bigscan = 1;
+  }
   if (frames && cap) {
     const uint64_t rc_n = region_entries(cap, nruns);
     const int rc = fmem_grow(s, 8 * (uint64_t)P.nflat * rc_n, cs != hipStreamCaptureStatusNone);
@@ -3297,35 +3278,7 @@ int stream_decode_fused(stream_scratch* s, uint8_t* base, uint64_t lo, uint64_t 
     P.fst = static_cast<uint64_t*>(s->fmem);
     P.rcap = rc_n;
   }
-  if (want_tab) {
-    // the table decoder (index, stream, descriptors); the run decoder after it
-    // reads the redirect record (the lattice scratch's) and takes what it left
-    tab_geom g;
-    const bool fits = small ? tab_geometry<G_TAB_SMALL>(s, hi, true, g) : tab_geometry<G_TAB>(s, hi, false, g);
-    if (fits) {
-      const bool capt = cs != hipStreamCaptureStatusNone;
-      if (const int rc = lat_grow(s, 1, capt)) return rc;
-      uint64_t doff, loff;
-      if (const int rc = tab_grow(s, tab_bytes(g, &doff, &loff), capt)) return rc;
-      run_params PT = P;
-      uint8_t* tm = static_cast<uint8_t*>(s->tmem);
-      PT.lat = static_cast<uint64_t*>(s->lmem);
-      PT.tctl = reinterpret_cast<uint64_t*>(tm);
-      PT.trec = reinterpret_cast<uint64_t*>(tm + 8 * TW_WORDS);
-      PT.tdesc = reinterpret_cast<uint4*>(tm + doff);
-      PT.tlist = reinterpret_cast<xyws_frame*>(tm + loff);
-      PT.trcap = g.rcap;
-      PT.tspr = g.spr;
-      PT.rbytes = g.spr * (small ? G_TAB_SMALL::SEG : G_TAB::SEG);
-      PT.nruns = (uint32_t)g.R;
-      PT.pfs = 0;
-      const int rc = small ? launch_table<G_SMALL, G_TAB_SMALL>(PT, g, 64, stream)
-                           : launch_table<G_PROD, G_TAB>(PT, g, (uint64_t)s->ncu, stream);
-      if (rc) return rc;
-      P.lat = PT.lat;
-      P.opts |= XYWS_OPT_REDIRECT;
-    }
-  } else if (want_lat) {
+  if (want_lat) {
     // the lattice decoder first; the run decoder after it reads its redirect
     // record. Its segment geometry (75 KiB for frames of LAT5_MIN_FRAME and
     // more, else 120 KiB), the first-segment gate and its bail-out after an

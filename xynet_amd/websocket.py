@@ -130,6 +130,10 @@ class Context:
     def reserve(self, max_batch_bytes, max_frames=0):
         check(self.L.xyws_ctx_reserve(self.h, max_batch_bytes, max_frames), "xyws_ctx_reserve")
 
+    def reserve_iov(self, max_total_bytes):
+        """xyws_ctx_reserve_iov: the buffer-sequence decode's staging buffer."""
+        check(self.L.xyws_ctx_reserve_iov(self.h, max_total_bytes), "xyws_ctx_reserve_iov")
+
     def last_device_error(self):
         """Device error word of the calls since the last read (0 = none);
         synchronizes the device and clears the word (xyws.h)."""
