@@ -1,7 +1,8 @@
-"""N > 1 bench path on the CPU (gloo, world size 2): each rank plans its own
-shard of independent frames (config 5) with no data exchange, and only the
-timing max and the parity AND cross ranks — the same helpers bench.py runs
-over RCCL on the GPU node."""
+"""N > 1 bench path on the CPU (gloo, world sizes 2 and 3): each rank plans
+its own shard of independent frames (config 5) with no data exchange, and
+only the timing max and the parity AND cross ranks — the same helpers and the
+same gloo group bench.py uses on the GPU node (it opens no RCCL communicator:
+the barrier and the reductions are a few bytes on the host)."""
 import json
 import os
 import socket

@@ -840,6 +840,45 @@ __global__ void __launch_bounds__(FT) k_rs_msgs(const xyws_frame* frames, const 
 // lane per 16-byte chunk, neighbours read for sequences crossing chunks.
 XYWS_DEV uint32_t lead_len(uint32_t c) { return c >= 0xF0u ? 4u : c >= 0xE0u ? 3u : c >= 0xC0u ? 2u : 0u; }
 
+// True when the bytes at out[] positions q in [q0, q1) of message [mo, me)
+// (out coordinates q = position - out_lo, total written) hold an invalid
+// UTF-8 sequence: k_utf8's per-byte rules (a continuation byte must be
+// claimed by a lead at most 3 bytes before it in the message; C0, C1 and
+// F5..FF never appear; a lead's continuations, overlongs, surrogates and
+// code points above U+10FFFF; a sequence cut by the message end is invalid
+// only in a complete, untruncated message). Byte loads: for the probe pass
+// (the first bytes of each message), not the streaming pass.
+XYWS_DEV bool utf8_span_bad(const uint8_t* out, uint64_t out_lo, uint64_t total, uint64_t q0, uint64_t q1,
+                            uint64_t mo, uint64_t me, uint32_t ty) {
+  for (uint64_t q = q0; q < q1 && q < me && q < total; q++) {
+    const uint32_t ch = out[out_lo + q];
+    if (ch < 0x80u) continue;
+    if (ch < 0xC0u) {
+      bool claimed = false;
+      for (uint32_t d = 1; d <= 3 && !claimed; d++) {
+        if (q < mo + d) break;
+        if (lead_len(out[out_lo + q - d]) > d) claimed = true;
+      }
+      if (!claimed) return true;
+    } else if (ch == 0xC0u || ch == 0xC1u || ch >= 0xF5u) {
+      return true;
+    } else {
+      const uint32_t L = lead_len(ch);
+      if (q + L > me || q + L > total) return (ty & XYWS_MSG_COMPLETE) && !(ty & XYWS_MSG_TRUNCATED);
+      uint32_t c1 = 0;
+      for (uint32_t d = 1; d < L; d++) {
+        const uint32_t cb = out[out_lo + q + d];
+        if ((cb & 0xC0u) != 0x80u) return true;
+        if (d == 1) c1 = cb;
+      }
+      if ((ch == 0xE0u && c1 < 0xA0u) || (ch == 0xEDu && c1 > 0x9Fu) || (ch == 0xF0u && c1 < 0x90u) ||
+          (ch == 0xF4u && c1 > 0x8Fu))
+        return true;
+    }
+  }
+  return false;
+}
+
 // UTF-8 tiles: UT bytes of out[] per tile; map[t] = the message holding the
 // tile's first byte (one lane per message marks its tiles, as k_tile_map
 // does for the gather), so a tile finds its messages with two loads and skips
@@ -870,6 +909,7 @@ struct ustage {
   uint32_t bad[UMS];
 };
 constexpr uint32_t UTEXT = 1u << 31;
+constexpr uint32_t UPROBE = 16;  // bytes of each message the probe pass checks
 
 __global__ void __launch_bounds__(FT) k_utf8(const uint8_t* out, uint64_t out_lo, uint64_t out_cap,
                                              const uint64_t* nmsg_p, xyws_message* msgs, uint64_t msg_cap,
@@ -918,6 +958,23 @@ __global__ void __launch_bounds__(FT) k_utf8(const uint8_t* out, uint64_t out_lo
       else atomicOr(&msgs[m].status, XYWS_MSG_UTF8_BAD);
     };
     if (s_text) {
+      // Probe pass: the first UPROBE bytes of each text message starting in
+      // the tile, one lane per message; a message found bad there is skipped
+      // by the streaming pass below before its loads (random "text", c1:
+      // every message is bad within its first bytes, so the tile's rows are
+      // never loaded — 64 lanes each checking their own chunk of a message's
+      // first row was 64 checks where one suffices)
+      {
+        const uint64_t tq0 = tile * UT > out_lo ? tile * UT - out_lo : 0;
+        for (uint64_t m = m0 + threadIdx.x; m <= m1; m += FT) {
+          const uint32_t ty = ty_of(m);
+          if (!(ty & UTEXT) || (ty & XYWS_MSG_UTF8_BAD)) continue;
+          const uint64_t mo = mo_of(m), me = me_of(m);
+          if (mo < tq0) continue;  // (its first bytes are an earlier tile's probe)
+          if (utf8_span_bad(out, out_lo, total, mo, mo + UPROBE, mo, me, ty)) mark(m, ty);
+        }
+        __syncthreads();
+      }
       // the tile's 16-byte chunks in out[] coordinates q = position - out_lo
       const uint64_t t0 = tile * UT;
       // each wave walks its own UT/4 bytes row by row (a row: 64 chunks, one
@@ -934,6 +991,20 @@ __global__ void __launch_bounds__(FT) k_utf8(const uint8_t* out, uint64_t out_lo
         const uint64_t q0 = a > out_lo ? a - out_lo : 0;
         if (q0 >= total) break;
         if (q0 >= sk0 && a + 16 - out_lo <= sk1) continue;
+        {
+          // (a chunk inside a message the probe found bad: no load)
+          uint64_t lo = m0, hi = m1 + 1;
+          while (hi - lo > 1) {
+            const uint64_t md = (lo + hi) >> 1;
+            if (mo_of(md) <= q0) lo = md; else hi = md;
+          }
+          const uint64_t q1 = a + 16 - out_lo;
+          if ((ty_of(lo) & XYWS_MSG_UTF8_BAD) && q1 <= me_of(lo)) {
+            sk0 = mo_of(lo);
+            sk1 = me_of(lo);
+            continue;
+          }
+        }
         // the chunk's bytes: one 16-byte load when it lies inside the written
         // range, else byte loads of the bytes that do (the rest read as 0)
         uint32_t w[4];
