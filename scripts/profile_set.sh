@@ -14,6 +14,7 @@
 #   host    PCIe-inclusive host paths on c3
 #   echo    the loopback echo harness at a few receive-buffer sizes
 #   small   small-batch (echo-sized) decode latency with descriptors
+#   valu    SQ_INSTS_VALU / SQ_WAVES of the §8(f) kernels on c2 encode and reassemble (one --pmc pass each)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 T=${TAG:-r04x}
@@ -53,4 +54,9 @@ if has echo; then
   for b in 262144 4194304; do step echo_$b 200 examples/echo_loopback --frames 200000 --buf $b; done
 fi
 has small && step small 300 python scripts/small_batch_stats.py
+if has valu; then
+  for op in encode reassemble; do
+    step valu_$op 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --kernel-trace -d $PWD/gpurun_out/${T}_valu_$op -o run --output-format csv -- python3 bench.py --config c2 --op $op --steps 3 --warmup 2 --no-cpu --no-ceiling
+  done
+fi
 echo "== done $T"
