@@ -759,7 +759,8 @@ __global__ void __launch_bounds__(FT) k_rs_marks(const xyws_frame* frames, uint6
 // 1 for members; orphan continuations raise orph[the next start's rank].
 __global__ void __launch_bounds__(FT) k_rs_sizes(const xyws_frame* frames, uint64_t n, const uint64_t* dev_n,
                                                  const uint64_t* a, const uint64_t* b, uint64_t* sz,
-                                                 uint64_t* cnt, uint64_t* orphan_flag) {
+                                                 uint64_t* cnt, uint64_t* orphan_flag, const uint64_t* rank,
+                                                 uint64_t* starts) {
   const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
   if (i >= n) return;
   const uint64_t ne = n_eff(n, dev_n);
@@ -777,34 +778,36 @@ __global__ void __launch_bounds__(FT) k_rs_sizes(const xyws_frame* frames, uint6
       }
     }
   }
+  // starts[m] = the first frame of message m for EVERY message (also past
+  // msg_cap: a record's length and frame count end at the next message's
+  // start), by rank (st[] exclusive-scanned: frame i starts a message when
+  // the rank steps after it)
+  if (i < ne) {
+    const uint64_t r = rank[i];
+    if (rank[i + 1] != r) starts[r] = i;
+  }
   sz[i] = s;
   cnt[i] = c;
   orphan_flag[i] = o;
 }
 
-// starts[m] = the first frame of message m for EVERY message (also past
-// msg_cap: a record's length and frame count end at the next message's
-// start), by rank (st[] exclusive-scanned: frame i starts a message when the
-// rank steps after it)
-__global__ void __launch_bounds__(FT) k_rs_first(uint64_t n, const uint64_t* dev_n, const uint64_t* rank,
-                                                 uint64_t* starts) {
-  const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
-  const uint64_t ne = n_eff(n, dev_n);
-  if (i >= ne) return;
-  const uint64_t r = rank[i];
-  if (rank[i + 1] != r) starts[r] = i;
-}
+constexpr uint32_t UT = 65536;  // UTF-8 tile: bytes of out[] (k_utf8)
 
 // each record from the offsets of its start and the next start (starts[]:
-// every message's first frame, k_rs_first); continuations after the last
+// every message's first frame, k_rs_sizes); continuations after the last
 // message's FIN with no message after them set bit 0x200 of the device error
-// word
+// word. With umap, also the UTF-8 tile map: umap[t] = the message holding
+// the first byte of UTF-8 tile t (UT bytes of out[]), written by the lanes of
+// the messages whose bytes start a tile (a 1 MiB message spans 16), so that a
+// tile finds its messages with two loads and skips at once when none of them
+// is a text message.
 __global__ void __launch_bounds__(FT) k_rs_msgs(const xyws_frame* frames, const uint64_t* dev_n, uint64_t n,
                                                 const uint64_t* nmsg_p,
                                                 const uint64_t* off, const uint64_t* cntoff, const uint64_t* b,
                                                 const uint64_t* starts, const uint64_t* orph_rank,
                                                 uint64_t out_cap, xyws_message* msgs, uint64_t msg_cap,
-                                                uint64_t* dev_nmsgs, uint32_t* err) {
+                                                uint64_t* dev_nmsgs, uint32_t* err, uint64_t* umap,
+                                                uint64_t utiles, uint64_t out_lo) {
   const uint64_t m = (uint64_t)blockIdx.x * FT + threadIdx.x;
   const uint64_t ne = n_eff(n, dev_n), nm = *nmsg_p;
   if (m == 0) {
@@ -834,6 +837,16 @@ __global__ void __launch_bounds__(FT) k_rs_msgs(const xyws_frame* frames, const 
   r[2] = off[s];
   r[3] = off[ns] - off[s];
   r[4] = (uint64_t)st | (op << 32);
+  if (umap) {
+    const uint64_t qs = off[s], qe = off[ns] < out_cap ? off[ns] : out_cap;
+    if (qs < qe) {
+      if (qs == 0) umap[0] = m;
+      uint64_t t = (qs + out_lo + UT - 1) / UT;
+      if (t == 0) t = 1;
+      const uint64_t t1 = (qe + out_lo + UT - 1) / UT;
+      for (; t < t1 && t < utiles; t++) umap[t] = m;
+    }
+  }
 }
 
 // UTF-8 (RFC 3629) over every text message's bytes in out[out_lo + ...]; one
@@ -877,26 +890,6 @@ XYWS_DEV bool utf8_span_bad(const uint8_t* out, uint64_t out_lo, uint64_t total,
     }
   }
   return false;
-}
-
-// UTF-8 tiles: UT bytes of out[] per tile; map[t] = the message holding the
-// tile's first byte (one lane per message marks its tiles, as k_tile_map
-// does for the gather), so a tile finds its messages with two loads and skips
-// at once when none of them is a text message.
-constexpr uint32_t UT = 65536;
-__global__ void __launch_bounds__(FT) k_utf8_map(const uint64_t* nmsg_p, const xyws_message* msgs,
-                                                 uint64_t msg_cap, uint64_t out_lo, uint64_t out_cap,
-                                                 uint64_t* map, uint64_t ntiles) {
-  const uint64_t m = (uint64_t)blockIdx.x * FT + threadIdx.x;
-  const uint64_t nm0 = *nmsg_p, nm = nm0 < msg_cap ? nm0 : msg_cap;
-  if (m >= nm) return;
-  const uint64_t qs = msgs[m].out_off, qe0 = qs + msgs[m].length, qe = qe0 < out_cap ? qe0 : out_cap;
-  if (qs >= qe) return;
-  if (qs == 0) map[0] = m;
-  uint64_t t = (qs + out_lo + UT - 1) / UT;
-  if (t == 0) t = 1;
-  const uint64_t t1 = (qe + out_lo + UT - 1) / UT;
-  for (; t < t1 && t < ntiles; t++) map[t] = m;
 }
 
 // The tile's messages (up to UMS) are staged in LDS with a bad flag each; a
@@ -1210,12 +1203,16 @@ int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, const 
   // each), block partials, totals
   const uint64_t w = n + 1, nb = (n + SB - 1) / SB + 1;
   const uint64_t ntiles = ((reinterpret_cast<uintptr_t>(dev_out) & 15) + out_cap + GTILE - 1) / GTILE + 1;
-  if ((rc = ensure_aux(sl, 8 * (6 * w + 3 * nb + 4 + ntiles), capt))) return rc;
+  const uint64_t utiles = ((reinterpret_cast<uintptr_t>(dev_out) & 15) + out_cap + UT - 1) / UT + 1;
+  if ((rc = ensure_aux(sl, 8 * (7 * w + 3 * nb + 4 + ntiles + utiles), capt))) return rc;
   uint64_t* A = static_cast<uint64_t*>(sl->aux_mem);
   uint64_t *a = A, *b = A + w, *st = A + 2 * w, *off = A + 3 * w, *cnt = A + 4 * w, *orph = A + 5 * w;
-  uint64_t* part = A + 6 * w;     // 3 * nb: one slice per scan of a group
+  uint64_t* starts = A + 6 * w;   // every message's first frame
+  uint64_t* part = A + 7 * w;     // 3 * nb: one slice per scan of a group
   uint64_t* tot = part + 3 * nb;  // tot[0]: bytes, tot[1]: messages, tot[2], tot[3]: scratch totals
   uint64_t* tmap = tot + 4;       // gather tile map
+  uint64_t* umap = tmap + ntiles; // UTF-8 tile map
+  const bool utf8 = (opts & XYWS_REASM_UTF8) && out_cap && msg_cap;
   const dim3 gn((uint32_t)((n + FT - 1) / FT > 0 ? (n + FT - 1) / FT : 1));
   if (n) {
     hipLaunchKernelGGL(k_rs_marks, gn, dim3(FT), 0, s, dev_frames, n, dev_n, a, b, st);
@@ -1228,22 +1225,18 @@ int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, const 
     return rc;
   if (n) {
     hipLaunchKernelGGL(k_rs_sizes, gn, dim3(FT), 0, s, dev_frames, n, dev_n, (const uint64_t*)a,
-                       (const uint64_t*)b, off, cnt, orph);
+                       (const uint64_t*)b, off, cnt, orph, (const uint64_t*)st, starts);
     if ((rc = hip_err(hipGetLastError()))) return rc;
   }
   // output offsets, frame counts and orphan counts
   if ((rc = scan3<scan3_spec<op_sum, false, true>, scan3_spec<op_sum, false, true>, scan3_spec<op_sum, false, true>>(
            scan3_args{{off, cnt, orph}, {tot + 0, tot + 2, tot + 3}}, n, part, s)))
     return rc;
-  if (n) {
-    // (a[] is free after k_rs_sizes: every message's first frame)
-    hipLaunchKernelGGL(k_rs_first, gn, dim3(FT), 0, s, n, dev_n, (const uint64_t*)st, a);
-    if ((rc = hip_err(hipGetLastError()))) return rc;
-  }
   hipLaunchKernelGGL(k_rs_msgs, gn, dim3(FT), 0, s, dev_frames, dev_n, n, (const uint64_t*)(tot + 1),
                      (const uint64_t*)off,
-                     (const uint64_t*)cnt, (const uint64_t*)b, (const uint64_t*)a, (const uint64_t*)orph,
-                     out_cap, dev_msgs, msg_cap, dev_nmsgs, ctx->err);
+                     (const uint64_t*)cnt, (const uint64_t*)b, (const uint64_t*)starts, (const uint64_t*)orph,
+                     out_cap, dev_msgs, msg_cap, dev_nmsgs, ctx->err, utf8 ? umap : nullptr, utiles,
+                     (uint64_t)(reinterpret_cast<uintptr_t>(dev_out) & 15));
   if ((rc = hip_err(hipGetLastError()))) return rc;
   const uintptr_t oa = reinterpret_cast<uintptr_t>(dev_out);
   const uintptr_t sa = reinterpret_cast<uintptr_t>(dev_src);
@@ -1269,13 +1262,10 @@ int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, const 
     hipLaunchKernelGGL(k_gather, dim3(grid_for(tiles, 1, 8192)), dim3(FT), 0, s, G, (const uint64_t*)tmap, ntiles);
     if ((rc = hip_err(hipGetLastError()))) return rc;
   }
-  if ((opts & XYWS_REASM_UTF8) && out_cap && msg_cap) {
-    // (the gather's tile map is done with: the messages' UTF-8 tile map in its place)
-    const uint64_t utiles = (G.out_lo + out_cap + UT - 1) / UT + 1;
-    hipLaunchKernelGGL(k_utf8_map, dim3((msg_cap + FT - 1) / FT), dim3(FT), 0, s, (const uint64_t*)(tot + 1),
-                       (const xyws_message*)dev_msgs, msg_cap, G.out_lo, out_cap, tmap, utiles);
+  if (utf8) {
+    // (the UTF-8 tile map: k_rs_msgs)
     hipLaunchKernelGGL(k_utf8, dim3(grid_for(utiles, 1, 4096)), dim3(FT), 0, s, (const uint8_t*)G.out, G.out_lo,
-                       out_cap, (const uint64_t*)(tot + 1), dev_msgs, msg_cap, (const uint64_t*)tmap, utiles);
+                       out_cap, (const uint64_t*)(tot + 1), dev_msgs, msg_cap, (const uint64_t*)umap, utiles);
     if ((rc = hip_err(hipGetLastError()))) return rc;
   }
   return XYWS_OK;
