@@ -859,18 +859,34 @@ XYWS_DEV uint32_t lead_len(uint32_t c) { return c >= 0xF0u ? 4u : c >= 0xE0u ? 3
 // claimed by a lead at most 3 bytes before it in the message; C0, C1 and
 // F5..FF never appear; a lead's continuations, overlongs, surrogates and
 // code points above U+10FFFF; a sequence cut by the message end is invalid
-// only in a complete, untruncated message). Byte loads: for the probe pass
-// (the first bytes of each message), not the streaming pass.
+// only in a complete, untruncated message). For the probe pass (the first
+// bytes of each message), not the streaming pass.
 XYWS_DEV bool utf8_span_bad(const uint8_t* out, uint64_t out_lo, uint64_t total, uint64_t q0, uint64_t q1,
                             uint64_t mo, uint64_t me, uint32_t ty) {
+  // (q1 - q0 <= 16: the bytes [q0 - 3, q0 + 19) the rules look at come from
+  // three aligned 16-byte lines loaded at once — one memory round trip, not
+  // one per byte; lines at or past the bytes written read as zero, and the
+  // rules never look past them)
+  const uint64_t A = (out_lo + (q0 >= 3 ? q0 - 3 : 0)) & ~15ull, lim = out_lo + total;
+  u32x4 L0 = {0u, 0u, 0u, 0u}, L1 = L0, L2 = L0;
+  if (A < lim) L0 = *reinterpret_cast<const u32x4*>(out + A);
+  if (A + 16 < lim) L1 = *reinterpret_cast<const u32x4*>(out + A + 16);
+  if (A + 32 < lim) L2 = *reinterpret_cast<const u32x4*>(out + A + 32);
+  auto pick = [](const u32x4& v, uint32_t k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; };
+  auto at = [&](uint64_t q) -> uint32_t {
+    const uint32_t i = (uint32_t)(out_lo + q - A), k = (i >> 2) & 3u;
+    const uint32_t d0 = pick(L0, k), d1 = pick(L1, k), d2 = pick(L2, k);
+    const uint32_t d = i < 16 ? d0 : i < 32 ? d1 : d2;  // (selects: no private array)
+    return (d >> (8u * (i & 3u))) & 0xFFu;
+  };
   for (uint64_t q = q0; q < q1 && q < me && q < total; q++) {
-    const uint32_t ch = out[out_lo + q];
+    const uint32_t ch = at(q);
     if (ch < 0x80u) continue;
     if (ch < 0xC0u) {
       bool claimed = false;
       for (uint32_t d = 1; d <= 3 && !claimed; d++) {
         if (q < mo + d) break;
-        if (lead_len(out[out_lo + q - d]) > d) claimed = true;
+        if (lead_len(at(q - d)) > d) claimed = true;
       }
       if (!claimed) return true;
     } else if (ch == 0xC0u || ch == 0xC1u || ch >= 0xF5u) {
@@ -880,7 +896,7 @@ XYWS_DEV bool utf8_span_bad(const uint8_t* out, uint64_t out_lo, uint64_t total,
       if (q + L > me || q + L > total) return (ty & XYWS_MSG_COMPLETE) && !(ty & XYWS_MSG_TRUNCATED);
       uint32_t c1 = 0;
       for (uint32_t d = 1; d < L; d++) {
-        const uint32_t cb = out[out_lo + q + d];
+        const uint32_t cb = at(q + d);
         if ((cb & 0xC0u) != 0x80u) return true;
         if (d == 1) c1 = cb;
       }
