@@ -338,6 +338,42 @@ def test_reassemble_text_utf8_fragments_split_inside_sequences(ws, oracle):
 
 
 @pytest.mark.gpu
+def test_reassemble_utf8_probe_window(ws, oracle):
+    """k_utf8's probe pass (a text message's first 16 bytes, and the 3 bytes
+    either side its rules read) and the streaming pass's skip of the messages
+    it marks: an invalid byte, an overlong or surrogate lead, an out-of-range
+    code point, a cut sequence, or a VALID 2/3/4-byte sequence, at every
+    position 0..23 of text messages of 1..40 bytes, some fragmented, some
+    crossing a 64 KiB UTF-8 tile boundary (records and bytes against the
+    oracle's)."""
+    from xynet_amd import _lib
+    rng = streams.SplitMix(0x0F)
+    wire = msg_streams._frame(rng, 0x82, bytes(65536 - 2000))  # (the text messages cross the first tile end)
+    seqs = [b"\x80", b"\xc0\xaf", b"\xe0\x80\x80", b"\xed\xa0\x80", b"\xf4\x90\x80\x80", b"\xff", b"\xe2\x82",
+            "\u00e9".encode(), "\u20ac".encode(), "\U0001d11e".encode()]
+    k = 0
+    for length in (1, 3, 15, 16, 17, 18, 19, 20, 24, 40):
+        for pos in range(min(length, 24)):
+            seq = seqs[k % len(seqs)]
+            k += 1
+            body = (b"x" * pos + seq + b"y" * length)[:length]
+            if k % 5 == 0 and length > 2:  # two fragments, cut inside the probe window
+                cut = rng.below(length)
+                wire += msg_streams._frame(rng, 0x01, body[:cut]) + msg_streams._frame(rng, 0x80, body[cut:])
+            else:
+                wire += msg_streams._frame(rng, 0x81, body)
+    t, frames_t, n, host, ofr = _decode(ws, oracle, wire)
+    oout, orecs = oracle.reassemble(host, ofr, _lib.REASM_UTF8)
+    out, mt, cnt = ws.reassemble(t, frames_t, n, _lib.REASM_UTF8)
+    nm = int(cnt.item())
+    assert nm == len(orecs)
+    got, want = _messages(mt, nm), [r.as_tuple() for r in orecs]
+    assert got == want
+    assert sum(1 for r in want if r[4] & 2) > 100 and sum(1 for r in want if r[5] == 1 and not r[4] & 2) > 30
+    assert out[:len(oout)].cpu().numpy().tobytes() == oout.tobytes()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["c2_bin_256", "c3_bin_64k"])
 def test_echo_round_trip_full_config(ws, name):
     """At a bench configuration: decode the batch, build client-role replies
