@@ -350,7 +350,7 @@ XYWS_DEV bool lat_redirect(run_params& P) {
   return true;
 }
 
-// Roles (as in the sweep decoder, sweep_io): in the production geometry wave
+// Roles (round 3's sweep decoder, retired, had the same split): in the production geometry wave
 // 0 is the CONTROL wave — claims, the covering frame's header and the 16 bytes
 // after the segment (loaded one segment ahead), the published results and the
 // look-back — and never loads or stores segment bytes, so its memory
@@ -430,7 +430,7 @@ XYWS_DEV uint32_t lat_ctrl_load(const run_params& P, uint64_t s, uint64_t SEGB, 
 // same four barriers per segment (A: LDS free, B: segment in LDS, C: table
 // and checks done, D: the look-back's answer), so the control wave's state
 // and the data waves' prefetch registers never share a register allocation
-// region (one loop holding both spilled the prefetch, as in sweep_loop).
+// region (one loop holding both spilled the prefetch in round 3's sweep decoder).
 enum { LR_ALL = 0, LR_CTRL = 1, LR_DATA = 2 };
 // stats mode (XYWS_OPT_STATS): shader clocks summed over workgroups, per phase,
 // for the control lane (tid 0) and one data lane (tid 64) — the debug stats
@@ -463,7 +463,7 @@ XYWS_DEV void lat_loop(const run_params& P, LL& L, uint32_t tid0, uint32_t ahead
   using IO = lat_io<G>;
   constexpr bool CT = ROLE != LR_DATA, DT = ROLE != LR_CTRL;
   uint32_t tid = tid0;
-  asm volatile("" : "+v"(tid));  // (lane address math per segment: see sweep_loop)
+  asm volatile("" : "+v"(tid));  // (opaque: hipcc would hoist the lane address math per segment and spill it)
   const uint32_t lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* cnt = reinterpret_cast<uint32_t*>(P.lat + LW_CNT);
@@ -511,7 +511,7 @@ XYWS_DEV void lat_loop(const run_params& P, LL& L, uint32_t tid0, uint32_t ahead
     ahead = a0;  // (claimed at the start)
     // K dropped stores (out-of-range offset, no traffic) after the first
     // loads, as after every later segment's: the fill's waits then count the
-    // stores younger than the loads on every path into the loop (sweep_loop)
+    // stores younger than the loads on every path into the loop
     const __amdgpu_buffer_rsrc_t rs = lat_rsrc(P, (uint64_t)cur * G::SEG, G::SEG);
 #pragma unroll
     for (uint32_t k = 0; k < IO::K; k++)

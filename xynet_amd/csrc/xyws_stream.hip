@@ -1075,8 +1075,8 @@ XYWS_DEV bool dense_pass(const run_params& P, lds_t<G>& L, uint64_t ss, uint32_t
   }
   // 3. validation and offsets (wave 0, one lane per sub-block)
   const bool cover = !(S0.st & (S_NOCOV | S_PARTCARRY)) && S0.X > ss;
-  // list entries before the frames: the covering frame, or (rsv0, the sweep
-  // decoder's speculative pass) a slot kept for the one the look-back supplies
+  // list entries before the frames: the covering frame, or (rsv0) a slot
+  // kept for one supplied later
   const uint32_t c0x = (cover || rsv0) ? 1u : 0u;
   if (tid < 64) {
     bool ok = true;
