@@ -120,14 +120,24 @@ XYWS_DEV uint64_t block_scan(uint64_t v, uint64_t* sh, uint64_t* exc, uint64_t* 
 template <class Op, bool Rev>
 XYWS_DEV uint64_t at(uint64_t n, uint64_t i) { return Rev ? n - 1 - i : i; }
 
-// pass 1: x[idx] <- the block-local scan (exclusive if Excl); part[b] <- total
-template <class Op, bool Rev, bool Excl>
-XYWS_DEV void scan_local(uint64_t* x, uint64_t n, uint64_t* part, uint64_t* sh) {
+// The values a scan starts from: x[] itself, or (a generator) computed from
+// the frame table in the scan's first pass, so that the per-frame pass that
+// produced them is not a launch of its own. val<K>(x, j): scan K's value at
+// index j.
+struct gen_load {
+  template <int K>
+  XYWS_DEV uint64_t val(const uint64_t* x, uint64_t j) const { return x[j]; }
+};
+
+// pass 1: x[idx] <- the block-local scan (exclusive if Excl) of the values
+// g gives; part[b] <- total
+template <class Op, bool Rev, bool Excl, int K = 0, class Gen = gen_load>
+XYWS_DEV void scan_local(uint64_t* x, uint64_t n, uint64_t* part, uint64_t* sh, const Gen& g = Gen()) {
   const uint64_t i0 = (uint64_t)blockIdx.x * SB + 4ull * threadIdx.x;
   uint64_t v[4], acc = Op::id();
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    v[k] = i0 + k < n ? x[at<Op, Rev>(n, i0 + k)] : Op::id();
+    v[k] = i0 + k < n ? g.template val<K>(x, at<Op, Rev>(n, i0 + k)) : Op::id();
     acc = Op::f(acc, v[k]);
   }
   uint64_t run, tot;
@@ -140,15 +150,15 @@ XYWS_DEV void scan_local(uint64_t* x, uint64_t n, uint64_t* part, uint64_t* sh) 
   }
   if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
-template <class Op, bool Rev, bool Excl>
-__global__ void __launch_bounds__(FT) k_scan_local(uint64_t* x, uint64_t n, uint64_t* part) {
+template <class Op, bool Rev, bool Excl, class Gen>
+__global__ void __launch_bounds__(FT) k_scan_local(uint64_t* x, uint64_t n, uint64_t* part, Gen g) {
   __shared__ uint64_t sh[FT / 64];
-  scan_local<Op, Rev, Excl>(x, n, part, sh);
+  scan_local<Op, Rev, Excl, 0, Gen>(x, n, part, sh, g);
 }
 
 // pass 2: one block scans the nb partials exclusively in place; *total <- all
 template <class Op>
-XYWS_DEV void scan_parts(uint64_t* part, uint64_t nb, uint64_t* total, uint64_t* sh) {
+XYWS_DEV void scan_parts(uint64_t* part, uint64_t nb, uint64_t* total, uint64_t* sh, uint64_t* total2 = nullptr) {
   uint64_t carry = Op::id();
   for (uint64_t c = 0; c < nb; c += FT) {
     const uint64_t i = c + threadIdx.x;
@@ -159,11 +169,12 @@ XYWS_DEV void scan_parts(uint64_t* part, uint64_t nb, uint64_t* total, uint64_t*
     carry = Op::f(carry, tot);
   }
   if (threadIdx.x == 0 && total) *total = carry;
+  if (threadIdx.x == 0 && total2) *total2 = carry;
 }
 template <class Op>
-__global__ void __launch_bounds__(FT) k_scan_parts(uint64_t* part, uint64_t nb, uint64_t* total) {
+__global__ void __launch_bounds__(FT) k_scan_parts(uint64_t* part, uint64_t nb, uint64_t* total, uint64_t* total2) {
   __shared__ uint64_t sh[FT / 64];
-  scan_parts<Op>(part, nb, total, sh);
+  scan_parts<Op>(part, nb, total, sh, total2);
 }
 
 // pass 3: x[idx] <- part[block] (op) x[idx]; exclusive scans also x[n] <- total
@@ -193,12 +204,12 @@ struct scan3_args {
   uint64_t* x[3];
   uint64_t* total[3];
 };
-template <class S0, class S1, class S2>
-__global__ void __launch_bounds__(FT) k_scan3_local(scan3_args A, uint64_t n, uint64_t* part, uint64_t nb) {
+template <class S0, class S1, class S2, class Gen>
+__global__ void __launch_bounds__(FT) k_scan3_local(scan3_args A, uint64_t n, uint64_t* part, uint64_t nb, Gen g) {
   __shared__ uint64_t sh[FT / 64];
-  scan_local<typename S0::Op, S0::Rev, S0::Excl>(A.x[0], n, part, sh);
-  scan_local<typename S1::Op, S1::Rev, S1::Excl>(A.x[1], n, part + nb, sh);
-  scan_local<typename S2::Op, S2::Rev, S2::Excl>(A.x[2], n, part + 2 * nb, sh);
+  scan_local<typename S0::Op, S0::Rev, S0::Excl, 0, Gen>(A.x[0], n, part, sh, g);
+  scan_local<typename S1::Op, S1::Rev, S1::Excl, 1, Gen>(A.x[1], n, part + nb, sh, g);
+  scan_local<typename S2::Op, S2::Rev, S2::Excl, 2, Gen>(A.x[2], n, part + 2 * nb, sh, g);
 }
 template <class S0, class S1, class S2>
 __global__ void __launch_bounds__(FT) k_scan3_parts(scan3_args A, uint64_t* part, uint64_t nb) {
@@ -214,30 +225,31 @@ __global__ void __launch_bounds__(FT) k_scan3_fix(scan3_args A, uint64_t n, cons
   scan_fix<typename S1::Op, S1::Rev, S1::Excl>(A.x[1], n, part + nb, A.total[1], i);
   scan_fix<typename S2::Op, S2::Rev, S2::Excl>(A.x[2], n, part + 2 * nb, A.total[2], i);
 }
-template <class S0, class S1, class S2>
-int scan3(const scan3_args& A, uint64_t n, uint64_t* part, hipStream_t s) {
+template <class S0, class S1, class S2, class Gen>
+int scan3(const scan3_args& A, uint64_t n, uint64_t* part, const Gen& g, hipStream_t s) {
   const uint64_t nb = (n + SB - 1) / SB;
-  if (nb) hipLaunchKernelGGL((k_scan3_local<S0, S1, S2>), dim3(nb), dim3(FT), 0, s, A, n, part, nb);
+  if (nb) hipLaunchKernelGGL((k_scan3_local<S0, S1, S2, Gen>), dim3(nb), dim3(FT), 0, s, A, n, part, nb, g);
   hipLaunchKernelGGL((k_scan3_parts<S0, S1, S2>), dim3(1), dim3(FT), 0, s, A, part, nb);
   hipLaunchKernelGGL((k_scan3_fix<S0, S1, S2>), dim3(nb ? (n + FT - 1) / FT : 1), dim3(FT), 0, s, A, n,
                      (const uint64_t*)part, nb);
   return hip_err(hipGetLastError());
 }
 
-// Scan n values in place (device memory x, n+1 words when Excl && total),
-// part: (n / SB + 1) words of scratch, total: device word (nullable).
-template <class Op, bool Rev, bool Excl>
-int scan(uint64_t* x, uint64_t n, uint64_t* part, uint64_t* total, hipStream_t s) {
+// Scan n values (from g) in place (device memory x, n+1 words when Excl &&
+// total), part: (n / SB + 1) words of scratch, total / total2: device words
+// (nullable) for the total.
+template <class Op, bool Rev, bool Excl, class Gen>
+int scan(uint64_t* x, uint64_t n, uint64_t* part, uint64_t* total, uint64_t* total2, const Gen& g, hipStream_t s) {
   const uint64_t nb = (n + SB - 1) / SB;
   if (nb == 0) {
     if (Excl && total) {
-      hipLaunchKernelGGL((k_scan_parts<Op>), dim3(1), dim3(FT), 0, s, part, 0ull, total);
+      hipLaunchKernelGGL((k_scan_parts<Op>), dim3(1), dim3(FT), 0, s, part, 0ull, total, total2);
       hipLaunchKernelGGL((k_scan_fix<Op, Rev, Excl>), dim3(1), dim3(FT), 0, s, x, 0ull, part, total);
     }
     return hip_err(hipGetLastError());
   }
-  hipLaunchKernelGGL((k_scan_local<Op, Rev, Excl>), dim3(nb), dim3(FT), 0, s, x, n, part);
-  hipLaunchKernelGGL((k_scan_parts<Op>), dim3(1), dim3(FT), 0, s, part, nb, total);
+  hipLaunchKernelGGL((k_scan_local<Op, Rev, Excl, Gen>), dim3(nb), dim3(FT), 0, s, x, n, part, g);
+  hipLaunchKernelGGL((k_scan_parts<Op>), dim3(1), dim3(FT), 0, s, part, nb, total, total2);
   hipLaunchKernelGGL((k_scan_fix<Op, Rev, Excl>), dim3((n + FT - 1) / FT), dim3(FT), 0, s, x, n,
                      (const uint64_t*)part, (const uint64_t*)total);
   return hip_err(hipGetLastError());
@@ -682,20 +694,21 @@ __global__ void __launch_bounds__(FT) k_gather(gparams G, const uint64_t* __rest
 }
 
 // ---------------------------------------------------------------- encode
-// sizes: header + payload of every selected frame (0 for the others)
-__global__ void __launch_bounds__(FT) k_enc_sizes(gparams G, const xyws_verdict* verd, uint32_t amask,
-                                                  uint64_t* sz) {
-  const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
-  if (i >= G.n) return;
-  const uint64_t ne = n_eff(G.n, G.dev_n);
-  uint64_t s = 0;
-  if (i < ne && (!verd || (amask >> verd[i].action) & 1u)) {
+// sizes: header + payload of every selected frame (0 for the others), made
+// in the offsets scan's first pass
+struct gen_enc {
+  gparams G;
+  const xyws_verdict* verd;
+  uint32_t amask;
+  template <int K>
+  XYWS_DEV uint64_t val(const uint64_t*, uint64_t i) const {
+    const uint64_t ne = n_eff(G.n, G.dev_n);
+    if (i >= ne || (verd && !((amask >> verd[i].action) & 1u))) return 0;
     const xyws_frame f = G.frames[i];
     uint32_t w[4];
-    s = build_header(reply_flags(G, f.flags), f.payload_len, false, 0, w) + f.payload_len;
+    return build_header(reply_flags(G, f.flags), f.payload_len, false, 0, w) + f.payload_len;
   }
-  sz[i] = s;
-}
+};
 
 // ---------------------------------------------------------------- classify
 __global__ void __launch_bounds__(FT) k_classify(const uint8_t* src, uint64_t src_len, const xyws_frame* frames,
@@ -734,24 +747,25 @@ __global__ void __launch_bounds__(FT) k_classify(const uint8_t* src, uint64_t sr
 }
 
 // ---------------------------------------------------------------- reassembly
-// a[i] = 1 + i for a text/binary frame (a message start), else 0; b[i] = i
-// for a data frame with FIN, else UINT64_MAX; st[i] = 1 for a start
-__global__ void __launch_bounds__(FT) k_rs_marks(const xyws_frame* frames, uint64_t n, const uint64_t* dev_n,
-                                                 uint64_t* a, uint64_t* b, uint64_t* st) {
-  const uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t ne = n_eff(n, dev_n);
-  uint64_t va = 0, vb = U64MAX, vs = 0;
-  if (i < ne) {
+// The first scan group's values (made in its first pass): a[i] = 1 + i for a
+// text/binary frame (a message start), else 0 (max-scanned: 1 + the last
+// start <= i); b[i] = i for a data frame with FIN, else UINT64_MAX
+// (min-scanned from the end: the next FIN >= i); st[i] = 1 for a start
+// (exclusive sum: message ranks).
+struct gen_marks {
+  const xyws_frame* frames;
+  uint64_t n;
+  const uint64_t* dev_n;
+  template <int K>
+  XYWS_DEV uint64_t val(const uint64_t*, uint64_t i) const {
+    if (i >= n_eff(n, dev_n)) return K == 1 ? U64MAX : 0;
     const uint32_t fl = frames[i].flags, op = fl & XYWS_FLAG_OP_MASK;
     const bool start = op == XYWS_FLAG_OP_TEXT || op == XYWS_FLAG_OP_BINARY;
-    if (start) { va = i + 1; vs = 1; }
-    if (op <= XYWS_FLAG_OP_BINARY && (fl & XYWS_FLAG_FIN)) vb = i;
+    if (K == 0) return start ? i + 1 : 0;
+    if (K == 1) return (op <= XYWS_FLAG_OP_BINARY && (fl & XYWS_FLAG_FIN)) ? i : U64MAX;
+    return start ? 1 : 0;
   }
-  a[i] = va;
-  b[i] = vb;
-  st[i] = vs;
-}
+};
 
 // After the scans: a[i] = 1 + the last start <= i (0: none), b[i] = the next
 // data frame with FIN >= i. Frame i belongs to the message of s = a[i] - 1
@@ -1167,14 +1181,9 @@ int xyws_encode_frames(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, con
   G.out_lo = oa & 15;
   G.out_cap = out_cap;
   G.err = ctx->err;
-  if (n) {
-    hipLaunchKernelGGL(k_enc_sizes, dim3((n + FT - 1) / FT), dim3(FT), 0, s, G, dev_verdicts, action_mask, off);
-    if ((rc = hip_err(hipGetLastError()))) return rc;
-  }
-  if ((rc = scan<op_sum, false, true>(off, n, part, total, s))) return rc;
-  if (dev_out_len) {
-    if ((rc = hip_err(hipMemcpyAsync(dev_out_len, total, 8, hipMemcpyDeviceToDevice, s)))) return rc;
-  }
+  // (the sizes made in the scan's first pass; the total also into dev_out_len)
+  if ((rc = scan<op_sum, false, true>(off, n, part, total, dev_out_len, gen_enc{G, dev_verdicts, action_mask}, s)))
+    return rc;
   if (n && out_cap) {
     const uint64_t tiles = (G.out_lo + out_cap + GTILE - 1) / GTILE;
     hipLaunchKernelGGL(k_tile_map, dim3((n + FT - 1) / FT), dim3(FT), 0, s, G, tmap, ntiles);
@@ -1230,23 +1239,21 @@ int xyws_reassemble(xyws_ctx* ctx, const void* dev_src, uint64_t src_len, const 
   uint64_t* umap = tmap + ntiles; // UTF-8 tile map
   const bool utf8 = (opts & XYWS_REASM_UTF8) && out_cap && msg_cap;
   const dim3 gn((uint32_t)((n + FT - 1) / FT > 0 ? (n + FT - 1) / FT : 1));
-  if (n) {
-    hipLaunchKernelGGL(k_rs_marks, gn, dim3(FT), 0, s, dev_frames, n, dev_n, a, b, st);
-    if ((rc = hip_err(hipGetLastError()))) return rc;
-  }
   // the last start at or before each frame, the next FIN at or after it, and
-  // the message ranks of the starts
+  // the message ranks of the starts (the marks made in the first pass)
   if ((rc = scan3<scan3_spec<op_max, false, false>, scan3_spec<op_min, true, false>, scan3_spec<op_sum, false, true>>(
-           scan3_args{{a, b, st}, {tot + 2, tot + 3, tot + 1}}, n, part, s)))
+           scan3_args{{a, b, st}, {tot + 2, tot + 3, tot + 1}}, n, part, gen_marks{dev_frames, n, dev_n}, s)))
     return rc;
+  // (the sizes in a kernel of their own: made inside the scan, each of its
+  // three values repeated the frame's random loads, c2 0.238 -> 0.307 ms)
   if (n) {
     hipLaunchKernelGGL(k_rs_sizes, gn, dim3(FT), 0, s, dev_frames, n, dev_n, (const uint64_t*)a,
                        (const uint64_t*)b, off, cnt, orph, (const uint64_t*)st, starts);
     if ((rc = hip_err(hipGetLastError()))) return rc;
   }
-  // output offsets, frame counts and orphan counts
+  // output offsets, frame counts and orphan ranks
   if ((rc = scan3<scan3_spec<op_sum, false, true>, scan3_spec<op_sum, false, true>, scan3_spec<op_sum, false, true>>(
-           scan3_args{{off, cnt, orph}, {tot + 0, tot + 2, tot + 3}}, n, part, s)))
+           scan3_args{{off, cnt, orph}, {tot + 0, tot + 2, tot + 3}}, n, part, gen_load{}, s)))
     return rc;
   hipLaunchKernelGGL(k_rs_msgs, gn, dim3(FT), 0, s, dev_frames, dev_n, n, (const uint64_t*)(tot + 1),
                      (const uint64_t*)off,
